@@ -1,0 +1,123 @@
+"""ctypes binding of the C ABI in ``include/fedavg_hip.h``.
+
+There is no CPU fallback: if the in-tree HIP library is missing or fails to load, every
+entry point raises. The symbols bound here are exactly the ones the header declares
+(``tests/test_abi.py`` checks that list against the header text).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, c_double, c_int32, c_int64, c_uint32, c_void_p
+from typing import Any
+
+from .build import LIB_PATH
+
+# enum fedavg_dtype
+F32, F16, BF16, F64 = 0, 1, 2, 3
+# enum fedavg_status
+OK = 0
+ERR_NAN_INPUT = 1
+ERR_NAN_ACCUM = 2
+ERR_NAN_RESULT = 3
+ERR_INVALID = 4
+ERR_HIP = 5
+ERR_STATE = 6
+FLAG_ACC_NAN = 0x1
+FLAG_RESULT_NAN = 0x2
+ABI_VERSION = 1
+
+_PP = POINTER(c_void_p)
+_PD = POINTER(c_double)
+
+# name -> (restype, argtypes); the full exported surface of the library
+SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
+    "fedavg_abi_version": (c_int32, []),
+    "fedavg_last_error": (ctypes.c_char_p, []),
+    "fedavg_ctx_create": (
+        c_int32,
+        [POINTER(c_void_p), c_int32, POINTER(c_int64), c_int32, c_void_p],
+    ),
+    "fedavg_ctx_destroy": (c_int32, [c_void_p]),
+    "fedavg_acc_numel": (c_int64, [c_void_p]),
+    "fedavg_segment_offset": (c_int64, [c_void_p, c_int32]),
+    "fedavg_accumulator": (c_void_p, [c_void_p]),
+    "fedavg_set_split_policy": (c_int32, [c_void_p, c_int32]),
+    "fedavg_reset": (c_int32, [c_void_p, c_void_p]),
+    "fedavg_total_weights": (c_int32, [c_void_p, _PD]),
+    "fedavg_accumulate": (c_int32, [c_void_p, _PP, c_int32, _PD, c_int32, c_void_p]),
+    "fedavg_aggregate": (
+        c_int32,
+        [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_int32, c_void_p],
+    ),
+    "fedavg_weighted_avg": (
+        c_int32,
+        [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_int32, c_void_p],
+    ),
+    "fedavg_partial": (
+        c_int32,
+        [c_void_p, _PP, c_int32, _PD, c_int32, c_int32, c_int32, c_int32, c_void_p],
+    ),
+    "fedavg_num_tiles": (c_int32, [c_void_p]),
+    "fedavg_tile_range": (
+        c_int32,
+        [c_void_p, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)],
+    ),
+    "fedavg_set_accumulated": (c_int32, [c_void_p, _PD]),
+    "fedavg_finalize_range": (
+        c_int32,
+        [c_void_p, _PP, c_int32, c_int32, c_int32, c_void_p],
+    ),
+    "fedavg_check": (c_int32, [c_void_p, c_void_p, POINTER(c_uint32)]),
+    "fedavg_find_nan_clients": (
+        c_int32,
+        [c_void_p, _PP, c_int32, c_int32, POINTER(c_int32), c_void_p],
+    ),
+    "fedavg_prof_enable": (c_int32, [c_void_p, c_int32]),
+    "fedavg_prof_collect": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
+    "fedavg_bw_probe": (c_int32, [c_void_p, c_int64, c_void_p, c_int32, c_void_p]),
+}
+
+_lib: ctypes.CDLL | None = None
+
+
+class NativeError(RuntimeError):
+    """A non-NaN failure reported by the HIP library."""
+
+    def __init__(self, status: int, message: str) -> None:
+        super().__init__(f"fedavg_hip status {status}: {message}")
+        self.status = status
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load the in-tree HIP library (raises if it is absent — there is no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    lib_path = path or str(LIB_PATH)
+    try:
+        lib = ctypes.CDLL(lib_path)
+    except OSError as e:
+        raise ImportError(
+            f"MI355X FedAvg library not loadable at {lib_path}: {e}. "
+            "Build it with `python -c 'import __graft_entry__ as g; g.build()'`."
+        ) from e
+    for name, (restype, argtypes) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    if lib.fedavg_abi_version() != ABI_VERSION:
+        raise ImportError("fedavg_hip ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().fedavg_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(status: int) -> None:
+    if status != OK:
+        raise NativeError(status, last_error())

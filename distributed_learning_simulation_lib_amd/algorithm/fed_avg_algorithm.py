@@ -1,0 +1,311 @@
+"""FedAvg on MI355X: the reference's streaming weighted average, folded in waves on the GPU.
+
+Same plugin surface as ``FedAVGAlgorithm`` in the reference
+(``simulation_lib/algorithm/fed_avg_algorithm.py:12-149``): ``accumulate`` /
+``aggregate_loss`` flags, the ``_accumulate_parameter`` / ``_get_weight`` /
+``_apply_total_weight`` / ``_aggregate_parameter`` hooks, ``process_worker_data`` /
+``aggregate_worker_data`` with the same message semantics.
+
+What differs is where the arithmetic happens. ``_accumulate_parameter`` stages each client
+tensor (moving it to the GPU if it arrived in host memory) instead of doing
+``acc += x.to(float64) * w`` on the CPU. Every ``wave_size`` clients the wave is folded into a
+device-resident fp64 accumulator by one HIP kernel launch, in arrival order, with separately
+rounded products and sums — bit-identical to the reference's fp64 sequence. The last wave is
+folded and divided by the total weight in the same launch (``fedavg_aggregate``), with the
+reference's NaN assertions fused into the kernel.
+
+Differences a caller can observe, all documented in DESIGN.md:
+  * the NaN assertions fire at the wave flush / aggregate, not at the offending arrival;
+  * ``aggregate_worker_data`` returns float64 tensors on the GPU (``result_device`` moves
+    them, e.g. to ``"cpu"`` as the reference's server does on caching);
+  * a key that first appears in a later client than the first one raises
+    ``NotImplementedError`` (the reference server always calls ``complete()`` first).
+"""
+
+from __future__ import annotations
+
+import os
+from collections.abc import MutableMapping
+from typing import Any
+
+import torch
+
+from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError
+from ..message import Message, ModelParameter, ParameterMessage
+from .aggregation_algorithm import (
+    AggregationAlgorithm,
+    default_device,
+    split_empty,
+    to_device_operand,
+    unify_dtype,
+)
+
+
+class FedAVGAlgorithm(AggregationAlgorithm):
+    def __init__(
+        self,
+        device: torch.device | str | None = None,
+        wave_size: int | None = None,
+        result_dtype: torch.dtype = torch.float64,
+        result_device: torch.device | str | None = None,
+        split_policy: int = 1,
+    ) -> None:
+        super().__init__()
+        self.accumulate: bool = True
+        self.aggregate_loss: bool = False
+        self._device = torch.device(device) if device is not None else None
+        self.wave_size = int(wave_size or os.environ.get("FEDAVG_WAVE_SIZE", 64))
+        assert self.wave_size >= 1
+        self.result_dtype = result_dtype
+        self.result_device = torch.device(result_device) if result_device is not None else None
+        self.split_policy = split_policy
+        self.__layout: ModelLayout | None = None
+        self.__native_layout: ModelLayout | None = None
+        self.__keep: list[int] = []
+        self.__ctx: FedAvgContext | None = None
+        self.__ctx_key: tuple | None = None
+        self.__table: ClientTable | None = None
+        self.__table_dtype: torch.dtype | None = None
+        self.__row: dict[str, tuple[torch.Tensor, Any]] = {}
+        self.__has_data = False
+
+    # ---- setup -------------------------------------------------------------------------
+    @property
+    def device(self) -> torch.device:
+        if self._device is None:
+            self._device = default_device()
+        return self._device
+
+    def _context(self) -> FedAvgContext:
+        assert self.__native_layout is not None
+        key = (self.device, self.__native_layout, self.split_policy)
+        if self.__ctx is None or self.__ctx_key != key:
+            if self.__ctx is not None:
+                self.__ctx.close()
+            self.__ctx = FedAvgContext(self.__native_layout, self.device, split_policy=self.split_policy)
+            self.__ctx_key = key
+        return self.__ctx
+
+    def _set_layout(self, parameter: ModelParameter) -> None:
+        self.__layout = ModelLayout.from_parameters(parameter)
+        self.__native_layout, self.__keep = split_empty(self.__layout)
+
+    # ---- per arrival (fed_avg_algorithm.py:20-41) --------------------------------------
+    def process_worker_data(
+        self,
+        worker_id: int,
+        worker_data: Message | None,
+    ) -> bool:
+        res = super().process_worker_data(worker_id=worker_id, worker_data=worker_data)
+        if not res:
+            return False
+        worker_data = self._all_worker_data.get(worker_id, None)
+        if worker_data is None:
+            return True
+        if not isinstance(worker_data, ParameterMessage):
+            return True
+        self.__row = {}
+        for name, parameter in worker_data.parameter.items():
+            self._accumulate_parameter(worker_data=worker_data, name=name, parameter=parameter)
+        if self.accumulate:
+            self._stage_client()
+        return True
+
+    def _accumulate_parameter(
+        self,
+        worker_data: ParameterMessage,
+        name: str,
+        parameter: torch.Tensor,
+    ) -> None:
+        """Stage (tensor, weight) for the next GPU wave; releases the payload like :64."""
+        if not self.accumulate:
+            return
+        weight = self._get_weight(worker_data=worker_data, name=name, parameter=parameter)
+        self.__row[name] = (to_device_operand(parameter, self.device), weight)
+        # release to reduce memory pressure (fed_avg_algorithm.py:63-64)
+        worker_data.parameter = {}
+
+    def _get_weight(self, worker_data: ParameterMessage, name: str, parameter: Any) -> Any:
+        return worker_data.aggregation_weight
+
+    def _apply_total_weight(self, name: str, parameter: torch.Tensor, total_weight: Any) -> torch.Tensor:
+        return parameter / total_weight
+
+    def _stage_client(self) -> None:
+        row = self.__row
+        self.__row = {}
+        if not row:
+            return
+        if self.__layout is None:
+            self._set_layout({k: v[0] for k, v in row.items()})
+        assert self.__layout is not None
+        unknown = [k for k in row if k not in self.__layout.names]
+        if unknown:
+            raise NotImplementedError(
+                f"tensors {unknown} were not in the first client's update; complete() the "
+                "message against the global model first (aggregation_server.py:126-128)"
+            )
+        if self.__native_layout is None:
+            self.__has_data = True
+            return
+        tensors: list[torch.Tensor | None] = []
+        weights: list[float] = []
+        for i in self.__keep:
+            name = self.__layout.names[i]
+            if name in row:
+                t, w = row[name]
+                if tuple(t.shape) != self.__layout.shapes[i]:
+                    raise ValueError(f"shape of {name} changed: {tuple(t.shape)} vs {self.__layout.shapes[i]}")
+                assert w is not None, "aggregation_weight is None"
+                tensors.append(t)
+                weights.append(float(w))
+            else:
+                tensors.append(None)
+                weights.append(0.0)
+        present = [t for t in tensors if t is not None]
+        if present:
+            unified, dt = unify_dtype(present)
+            it = iter(unified)
+            tensors = [next(it) if t is not None else None for t in tensors]
+        else:
+            dt = self.__table_dtype or torch.float32
+        if self.__table is not None and self.__table_dtype != dt:
+            self._flush()
+        if self.__table is None:
+            self.__table = ClientTable(len(self.__keep))
+            self.__table_dtype = dt
+        self.__table.add_client(tensors, weights)
+        self.__has_data = True
+        if self.__table.num_clients >= self.wave_size:
+            self._flush()
+
+    def _flush(self) -> None:
+        """Fold the staged wave into the device accumulator (one kernel launch)."""
+        if self.__table is None or self.__table.num_clients == 0:
+            return
+        ctx = self._context()
+        table, dt = self.__table, self.__table_dtype
+        assert dt is not None
+        self.__table, self.__table_dtype = None, None
+        ctx.accumulate(table, dt)
+
+    # ---- end of round (fed_avg_algorithm.py:76-113) ------------------------------------
+    def _aggregate_parameter(self, chosen_worker_ids: set[int] | None = None) -> ModelParameter:
+        if not self.accumulate:
+            worker_data: MutableMapping[int, Message] = self._all_worker_data
+            if chosen_worker_ids is not None:
+                worker_data = {k: worker_data[k] for k in chosen_worker_ids}
+            return AggregationAlgorithm.weighted_avg(
+                worker_data, AggregationAlgorithm.get_ratios(worker_data), device=self.device
+            )
+        assert self.__has_data
+        assert chosen_worker_ids is None
+        layout = self.__layout
+        assert layout is not None
+        result: ModelParameter = {}
+        if self.__native_layout is not None:
+            result.update(self._finish_native())
+        for i, name in enumerate(layout.names):
+            if i not in self.__keep:
+                result[name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
+        self.__has_data = False
+        out = {name: result[name] for name in layout.names}
+        if self.result_device is not None:
+            out = {k: v.to(self.result_device) for k, v in out.items()}
+        return out
+
+    def _finish_native(self) -> ModelParameter:
+        ctx = self._context()
+        native = self.__native_layout
+        layout = self.__layout
+        assert native is not None and layout is not None
+        table, dt = self.__table, self.__table_dtype
+        self.__table, self.__table_dtype = None, None
+        pending = [(table, dt)] if table is not None and dt is not None else []
+        custom_divide = type(self)._apply_total_weight is not FedAVGAlgorithm._apply_total_weight
+        out_dtype = torch.float64 if custom_divide else self.result_dtype
+        flat = torch.empty(native.padded_offsets(8 if out_dtype == torch.float64 else 4)[1],
+                           dtype=out_dtype, device=self.device)
+        offs, _ = native.padded_offsets(flat.element_size())
+        outs = [flat[o : o + n] for o, n in zip(offs, native.numels)]
+        try:
+            if not custom_divide:
+                ctx.aggregate(table, dt or torch.float32, outs, out_dtype)
+                ctx.raise_on_nan(pending)
+            else:
+                # a subclass divides: finalize with a unit divisor (exact), then call its hook
+                if table is not None and dt is not None:
+                    ctx.accumulate(table, dt)
+                totals = ctx.total_weights()
+                ctx.set_accumulated([1.0] * native.num_segments)
+                ctx.finalize_range(outs, torch.float64)
+                ctx.raise_on_nan(pending)
+        except NaNAggregationError:
+            ctx.reset()
+            raise
+        result: ModelParameter = {}
+        for j, i in enumerate(self.__keep):
+            name = layout.names[i]
+            value = outs[j].view(layout.shapes[i])
+            if custom_divide:
+                value = self._apply_total_weight(name=name, parameter=value, total_weight=totals[j])
+                assert not value.isnan().any().cpu()
+                value = value.to(self.result_dtype)
+            result[name] = value
+        ctx.reset()
+        return result
+
+    def aggregate_worker_data(self) -> ParameterMessage:
+        parameter = self._aggregate_parameter()
+        other_data: dict[str, Any] = {}
+        if self.aggregate_loss:
+            other_data |= self.__aggregate_loss(self._all_worker_data)
+        other_data |= self.__check_and_reduce_other_data(self._all_worker_data)
+        first = next(iter(self._all_worker_data.values()))
+        return ParameterMessage(
+            parameter=parameter,
+            end_training=first.end_training,
+            in_round=first.in_round,
+            other_data=other_data,
+        )
+
+    def clear_worker_data(self) -> None:
+        super().clear_worker_data()
+        self.__table, self.__table_dtype = None, None
+        self.__row = {}
+        self.__has_data = False
+        if self.__ctx is not None:
+            self.__ctx.reset()
+
+    def exit(self) -> None:
+        if self.__ctx is not None:
+            self.__ctx.close()
+            self.__ctx = None
+
+    @classmethod
+    def __aggregate_loss(cls, all_worker_data: MutableMapping[int, Message]) -> dict[str, Any]:
+        """Ratio-weighted training/validation loss (fed_avg_algorithm.py:115-134)."""
+        assert all_worker_data
+        first = next(iter(all_worker_data.values()))
+        loss_types = [t for t in ("training_loss", "validation_loss") if t in first.other_data]
+        ratios = AggregationAlgorithm.get_ratios(all_worker_data)
+        loss_dict = {
+            t: AggregationAlgorithm.weighted_avg_for_scalar(all_worker_data, ratios, scalar_key=t)
+            for t in loss_types
+        }
+        assert loss_dict
+        for msg in all_worker_data.values():
+            for t in ("training_loss", "validation_loss"):
+                msg.other_data.pop(t, None)
+        return loss_dict
+
+    @classmethod
+    def __check_and_reduce_other_data(cls, all_worker_data: MutableMapping[int, Message]) -> dict[str, Any]:
+        """Every client must agree on every other_data key (fed_avg_algorithm.py:136-149)."""
+        merged: dict[str, Any] = {}
+        for msg in all_worker_data.values():
+            for k, v in msg.other_data.items():
+                if k in merged and v != merged[k]:
+                    raise RuntimeError(f"different values on key {k}")
+                merged.setdefault(k, v)
+        return merged

@@ -1,0 +1,68 @@
+"""Build the gfx950 HIP library in-tree (``_lib/libfedavg_hip.so``).
+
+The library is the C-ABI declared in ``include/fedavg_hip.h``. It is compiled with
+``hipcc --offload-arch=gfx950`` straight from ``csrc/`` — no torch extension machinery, no
+JIT cache: the built ``.so`` lives next to the package so it travels with the repository
+snapshot to the GPU box.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+CSRC = PKG_DIR / "csrc"
+LIB_DIR = PKG_DIR / "_lib"
+LIB_NAME = "libfedavg_hip.so"
+LIB_PATH = LIB_DIR / LIB_NAME
+SOURCES = [CSRC / "fedavg_kernels.hip"]
+HEADERS = [REPO_DIR / "include" / "fedavg_hip.h"]
+
+# -ffp-contract=off: the reference rounds the fp64 product and the fp64 sum separately
+# (torch `x.to(f64) * w` then `acc += tmp`); an FMA would change low bits.
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-ffp-contract=off",
+    "-fPIC",
+    "-shared",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def hipcc() -> str:
+    cand = os.environ.get("HIPCC") or shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    return cand
+
+
+def needs_build() -> bool:
+    if not LIB_PATH.exists():
+        return True
+    mtime = LIB_PATH.stat().st_mtime
+    return any(p.stat().st_mtime > mtime for p in SOURCES + HEADERS + [Path(__file__)])
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the HIP library for gfx950. Returns the path of the shared object."""
+    if not force and not needs_build():
+        return LIB_PATH
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc(), *HIPCC_FLAGS, f"-I{REPO_DIR / 'include'}", *map(str, SOURCES), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd))
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,1244 @@
+// fedavg_kernels.hip — gfx950 (MI355X) kernels of the server-side weighted FedAvg reduce.
+//
+// What the reference computes (simulation_lib/algorithm/fed_avg_algorithm.py:43-99):
+//   for every arriving client k, for every named tensor t:
+//       tmp = x_k[t].to(float64) * w_k          (:54)
+//       acc[t] = tmp            if first else acc[t] += tmp   (:55-58)
+//       W[t]  += w_k                                         (:59-62)
+//   at the end: assert !isnan(acc[t]); out[t] = acc[t] / W[t]; assert !isnan(out[t]) (:92-97)
+//
+// How it is laid out here:
+//   * A model is T segments (its named tensors). Every segment is cut into tiles of TILE
+//     elements (never crossing a segment). One workgroup owns one tile and streams that
+//     tile's slice of every client bucket from HBM, 16 B per lane per load, CU_LOADS clients
+//     in flight per lane, accumulating in fp64 registers in client order. The fp64 product
+//     and the fp64 sum are separately rounded (-ffp-contract=off), so each element's value
+//     is bit-identical to the reference's torch CPU ops.
+//   * SPLIT=4 variant (small-P / large-N shapes): the four waves of a workgroup take four
+//     contiguous client ranges of the same 512-element tile; wave partials are staged in LDS
+//     and wave 0 combines them in wave order (deterministic, but a different fp64 order).
+//   * The NaN assertions are fused: one isnan per accumulated element, a wavefront ballot,
+//     and one atomicOr per wave that saw a NaN.
+//   * No MFMA: 0.25-0.5 flop per byte, the kernel is HBM-bound.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fedavg_hip.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------------------
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define FEDAVG_HIP_TRY(expr)                                                              \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      return fail(FEDAVG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    }                                                                                     \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------
+// device-side descriptors
+// ---------------------------------------------------------------------------------------
+constexpr int kThreads = 256;     // 4 waves of 64
+constexpr int kAE = 8;            // elements owned by one lane (fp64 accumulators per lane)
+constexpr int kTile1 = kThreads * kAE;        // 2048 elements, SPLIT = 1
+constexpr int kTile4 = (kThreads / 4) * kAE;  // 512 elements,  SPLIT = 4
+
+struct TileDesc {
+  int32_t seg;
+  int32_t count;   // elements in this tile (== tile size except at a segment's end)
+  int64_t start;   // first element, relative to the segment
+};
+
+struct SegDesc {
+  int64_t acc_off;  // offset of the segment in the padded fp64 accumulator
+  int64_t numel;
+};
+
+// Per-call table blob (device copy of a pinned staging slot). Segment-major so that the
+// clients of one tile are contiguous for scalar loads.
+struct CallTables {
+  const void* const* cptrs;  // [T][K] compacted (non-null) client pointers
+  const double* w;           // [T][K] weights
+  const int32_t* kseg;       // [T] number of clients for the segment in this call
+  const int32_t* acc_in;     // [T] 1 = accumulator holds data for the segment
+  void* const* outs;         // [T] output pointers (final kernels)
+  const double* wtot;        // [T] divisor (final kernels)
+};
+
+struct KArgs {
+  const TileDesc* tiles;
+  const SegDesc* segs;
+  CallTables tab;
+  double* acc;
+  uint32_t* flag;
+  int32_t tile_begin;
+  int32_t K;           // row stride of the [T][K] tables
+  int32_t zero_init;   // start every segment at +0.0 (shard partials)
+};
+
+enum OutKind : int { OUT_ACC = 0, OUT_F32 = 1, OUT_F64 = 2 };
+
+// Clang ext-vector types: builtin vector values, usable through address-space-qualified
+// pointers (HIP's struct vector types are not).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte vector of the input type
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<float> {
+  using type = f32x4;
+  static constexpr int n = 4;
+};
+template <>
+struct Vec16<double> {
+  using type = f64x2;
+  static constexpr int n = 2;
+};
+template <>
+struct Vec16<__half> {
+  using type = u32x4;  // 8 halves
+  static constexpr int n = 8;
+};
+struct bf16_t {
+  uint16_t bits;
+};
+template <>
+struct Vec16<bf16_t> {
+  using type = u32x4;  // 8 bf16
+  static constexpr int n = 8;
+};
+
+__device__ __forceinline__ double to_f64(float x) { return static_cast<double>(x); }
+__device__ __forceinline__ double to_f64(double x) { return x; }
+__device__ __forceinline__ double half_bits_to_f64(uint32_t h) {
+  return static_cast<double>(__half2float(__ushort_as_half(static_cast<unsigned short>(h))));
+}
+__device__ __forceinline__ double bf16_bits_to_f64(uint32_t b) {
+  return static_cast<double>(__uint_as_float(b << 16));
+}
+
+// Expand one 16-byte vector into Vec16<T>::n doubles.
+template <typename T>
+__device__ __forceinline__ void expand(const typename Vec16<T>::type& v, double* out);
+template <>
+__device__ __forceinline__ void expand<float>(const f32x4& v, double* o) {
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void expand<double>(const f64x2& v, double* o) {
+  o[0] = v.x; o[1] = v.y;
+}
+template <>
+__device__ __forceinline__ void expand<__half>(const u32x4& v, double* o) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = half_bits_to_f64(w[i] & 0xffffu);
+    o[2 * i + 1] = half_bits_to_f64(w[i] >> 16);
+  }
+}
+template <>
+__device__ __forceinline__ void expand<bf16_t>(const u32x4& v, double* o) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = bf16_bits_to_f64(w[i] & 0xffffu);
+    o[2 * i + 1] = bf16_bits_to_f64(w[i] >> 16);
+  }
+}
+
+// scalar element load
+template <typename T>
+__device__ __forceinline__ double load_elem(const T* p, int64_t i);
+template <>
+__device__ __forceinline__ double load_elem<float>(const float* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ double load_elem<double>(const double* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ double load_elem<__half>(const __half* p, int64_t i) {
+  return half_bits_to_f64(reinterpret_cast<const uint16_t*>(p)[i]);
+}
+template <>
+__device__ __forceinline__ double load_elem<bf16_t>(const bf16_t* p, int64_t i) {
+  return bf16_bits_to_f64(reinterpret_cast<const uint16_t*>(p)[i]);
+}
+
+// Address-space-qualified pointers. Client buffers and outputs are read and written through
+// the global address space (saddr `global_load_dwordx4 v, v_off, s[base]`, never `flat_`);
+// per-call tables are read through the constant address space, which makes every
+// wave-uniform table read a scalar `s_load` (8 client pointers per s_load_dwordx16).
+#define FEDAVG_AS_GLOBAL __attribute__((address_space(1)))
+#define FEDAVG_AS_CONST __attribute__((address_space(4)))
+template <typename T>
+using gptr = T FEDAVG_AS_GLOBAL*;
+template <typename T>
+using kptr = const T FEDAVG_AS_CONST*;
+
+template <typename T>
+__device__ __forceinline__ gptr<const T> to_global(const void* p) {
+  return (gptr<const T>)(p);
+}
+template <typename T>
+__device__ __forceinline__ gptr<T> to_global_mut(void* p) {
+  return (gptr<T>)(p);
+}
+template <typename T>
+__device__ __forceinline__ kptr<T> to_const(const void* p) {
+  return (kptr<T>)(p);
+}
+
+// scalar (s_load) read of a tile descriptor
+__device__ __forceinline__ TileDesc load_tile(const TileDesc* tiles, int64_t i) {
+  const kptr<int32_t> p = to_const<int32_t>(tiles + i);
+  TileDesc d;
+  d.seg = p[0];
+  d.count = p[1];
+  d.start = to_const<int64_t>(tiles + i)[1];
+  return d;
+}
+
+template <typename T>
+__device__ __forceinline__ double load_g(gptr<const T> p, int64_t i);
+template <>
+__device__ __forceinline__ double load_g<float>(gptr<const float> p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ double load_g<double>(gptr<const double> p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ double load_g<__half>(gptr<const __half> p, int64_t i) {
+  return half_bits_to_f64(((gptr<const uint16_t>)p)[i]);
+}
+template <>
+__device__ __forceinline__ double load_g<bf16_t>(gptr<const bf16_t> p, int64_t i) {
+  return bf16_bits_to_f64(((gptr<const uint16_t>)p)[i]);
+}
+
+// Loads of one client's share of a tile for one lane: VPL vectors of 16 B, expanded to
+// kAE doubles. Element index (within the tile) of vector v of lane li: (v*LANES + li)*N,
+// so one wave-instruction reads 1 KiB contiguous.
+template <typename T, int LANES, bool FULL, bool VEC>
+struct LaneLoader {
+  using V = typename Vec16<T>::type;
+  static constexpr int N = Vec16<T>::n;
+  static constexpr int VPL = kAE / N;
+
+  // raw 16-B loads (fast path: whole tile, aligned buffers)
+  __device__ __forceinline__ static void load_raw(gptr<const T> base, int li, V (&buf)[VPL]) {
+    const gptr<const V> vb = (gptr<const V>)base;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) buf[v] = vb[v * LANES + li];
+  }
+
+  // bounds-checked loads straight to doubles (segment tails, unaligned buffers)
+  __device__ __forceinline__ static void load_checked(gptr<const T> base, int li, int count,
+                                                      double (&x)[kAE]) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+      if (VEC && e + N <= count) {
+        const V raw = ((gptr<const V>)base)[v * LANES + li];
+        expand<T>(raw, x + v * N);
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) x[v * N + j] = (e + j < count) ? load_g<T>(base, e + j) : 0.0;
+      }
+    }
+  }
+};
+
+// One tile of the weighted reduce. See the file header for the algorithm.
+template <typename T, int OUT, int SPLIT, bool VEC, bool FULL>
+__device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
+  constexpr int LANES = kThreads / SPLIT;  // lanes sharing one client stream
+  using LL = LaneLoader<T, LANES, FULL && VEC, VEC>;
+  using V = typename LL::V;
+  constexpr int N = LL::N;
+  constexpr int VPL = LL::VPL;
+  // clients in flight per lane: 256 B of loads per lane per group
+  constexpr int CU_LOADS = (256 / (VPL * 16)) < 2 ? 2 : (256 / (VPL * 16));
+  constexpr bool FAST = FULL && VEC;
+
+  const int seg = td.seg;
+  const int count = td.count;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int li = (SPLIT == 1) ? static_cast<int>(threadIdx.x) : static_cast<int>(threadIdx.x & 63);
+
+  const int kseg = to_const<int32_t>(a.tab.kseg)[seg];
+  int kb = 0, ke = kseg;
+  if constexpr (SPLIT > 1) {
+    const int per = (kseg + SPLIT - 1) / SPLIT;
+    kb = min(kseg, wave * per);
+    ke = min(kseg, kb + per);
+  }
+  const kptr<uint64_t> cp = to_const<uint64_t>(a.tab.cptrs) + static_cast<int64_t>(seg) * a.K;
+  const kptr<double> wp = to_const<double>(a.tab.w) + static_cast<int64_t>(seg) * a.K;
+  const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;  // SegDesc::acc_off
+  const int64_t elem_off = td.start * static_cast<int64_t>(sizeof(T));
+  auto client = [&](int k) -> gptr<const T> {
+    return to_global<T>(reinterpret_cast<const void*>(cp[k] + elem_off));
+  };
+
+  double acc[kAE];
+  bool have = false;  // wave-uniform
+  if (SPLIT == 1 || wave == 0) {
+    if (a.zero_init) {
+#pragma unroll
+      for (int i = 0; i < kAE; ++i) acc[i] = 0.0;
+      have = true;
+    } else if (to_const<int32_t>(a.tab.acc_in)[seg]) {
+      const gptr<const double> ap = to_global<double>(a.acc + acc_base);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const int e = (v * LANES + li) * N;
+#pragma unroll
+        for (int j = 0; j < N; j += 2) {
+          if (FULL || e + j + 2 <= count) {
+            const f64x2 d = *(gptr<const f64x2>)(ap + e + j);
+            acc[v * N + j] = d.x;
+            acc[v * N + j + 1] = d.y;
+          } else {
+            acc[v * N + j] = (e + j < count) ? ap[e + j] : 0.0;
+            acc[v * N + j + 1] = (e + j + 1 < count) ? ap[e + j + 1] : 0.0;
+          }
+        }
+      }
+      have = true;
+    }
+  }
+
+  int k = kb;
+  if (!have && k < ke) {
+    // first contribution is an assignment (fed_avg_algorithm.py:55-56), not 0 + tmp
+    const double wk = wp[k];
+    double x[kAE];
+    if constexpr (FAST) {
+      V buf[VPL];
+      LL::load_raw(client(k), li, buf);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) expand<T>(buf[v], x + v * N);
+    } else {
+      LL::load_checked(client(k), li, count, x);
+    }
+#pragma unroll
+    for (int i = 0; i < kAE; ++i) acc[i] = x[i] * wk;
+    have = true;
+    ++k;
+  }
+  if constexpr (FAST) {
+    // main loop: CU_LOADS clients' loads in flight, then fold them in client order
+    for (; k + CU_LOADS <= ke; k += CU_LOADS) {
+      V buf[CU_LOADS][VPL];
+      double wk[CU_LOADS];
+#pragma unroll
+      for (int c = 0; c < CU_LOADS; ++c) {
+        wk[c] = wp[k + c];
+        LL::load_raw(client(k + c), li, buf[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < CU_LOADS; ++c) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          double x[N];
+          expand<T>(buf[c][v], x);
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            const double prod = x[j] * wk[c];
+            acc[v * N + j] = acc[v * N + j] + prod;
+          }
+        }
+      }
+    }
+    for (; k < ke; ++k) {
+      const double wk = wp[k];
+      V buf[VPL];
+      LL::load_raw(client(k), li, buf);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        double x[N];
+        expand<T>(buf[v], x);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const double prod = x[j] * wk;
+          acc[v * N + j] = acc[v * N + j] + prod;
+        }
+      }
+    }
+  } else {
+    for (; k < ke; ++k) {
+      const double wk = wp[k];
+      double x[kAE];
+      LL::load_checked(client(k), li, count, x);
+#pragma unroll
+      for (int i = 0; i < kAE; ++i) {
+        const double prod = x[i] * wk;
+        acc[i] = acc[i] + prod;
+      }
+    }
+  }
+
+  if constexpr (SPLIT > 1) {
+    // stage wave partials in LDS; wave 0 folds them in wave order
+    int* have_lds = reinterpret_cast<int*>(lds + (SPLIT - 1) * 64 * kAE);
+    if (wave > 0) {
+      double* dst = lds + ((wave - 1) * 64 + li) * kAE;
+#pragma unroll
+      for (int i = 0; i < kAE; ++i) dst[i] = acc[i];
+      if (li == 0) have_lds[wave - 1] = have ? 1 : 0;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int w2 = 1; w2 < SPLIT; ++w2) {
+      if (have_lds[w2 - 1]) {
+        const double* src = lds + ((w2 - 1) * 64 + li) * kAE;
+        if (have) {
+#pragma unroll
+          for (int i = 0; i < kAE; ++i) acc[i] = acc[i] + src[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < kAE; ++i) acc[i] = src[i];
+        }
+        have = true;
+      }
+    }
+  }
+  if (!have) return;  // nothing for this segment in this call (host prevents for finals)
+
+  // fused NaN check on the accumulator (fed_avg_algorithm.py:93)
+  bool bad_acc = false;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = (v * LANES + li) * N;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const bool in_range = FULL || (e + j < count);
+      bad_acc |= in_range && (acc[v * N + j] != acc[v * N + j]);
+    }
+  }
+
+  if constexpr (OUT == OUT_ACC) {
+    const gptr<double> ap = to_global_mut<double>(a.acc + acc_base);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+#pragma unroll
+      for (int j = 0; j < N; j += 2) {
+        if (FULL || e + j + 2 <= count) {
+          *(gptr<f64x2>)(ap + e + j) = f64x2{acc[v * N + j], acc[v * N + j + 1]};
+        } else {
+          if (e + j < count) ap[e + j] = acc[v * N + j];
+          if (e + j + 1 < count) ap[e + j + 1] = acc[v * N + j + 1];
+        }
+      }
+    }
+    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) atomicOr(a.flag, FEDAVG_FLAG_ACC_NAN);
+  } else {
+    // fused divide (_apply_total_weight, :71-74) + NaN check of the result (:97)
+    const double W = to_const<double>(a.tab.wtot)[seg];
+    bool bad_res = false;
+    double res[kAE];
+#pragma unroll
+    for (int i = 0; i < kAE; ++i) res[i] = acc[i] / W;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const bool in_range = FULL || (e + j < count);
+        bad_res |= in_range && (res[v * N + j] != res[v * N + j]);
+      }
+    }
+    void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
+    if constexpr (OUT == OUT_F32) {
+      const gptr<float> op = to_global_mut<float>(out_raw) + td.start;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const int e = (v * LANES + li) * N;
+        if constexpr (N >= 4) {
+#pragma unroll
+          for (int j = 0; j < N; j += 4) {
+            if (VEC && (FULL || e + j + 4 <= count)) {
+              *(gptr<f32x4>)(op + e + j) =
+                  f32x4{static_cast<float>(res[v * N + j]), static_cast<float>(res[v * N + j + 1]),
+                        static_cast<float>(res[v * N + j + 2]), static_cast<float>(res[v * N + j + 3])};
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (e + j + q < count) op[e + j + q] = static_cast<float>(res[v * N + j + q]);
+            }
+          }
+        } else {
+          if (VEC && (FULL || e + 2 <= count)) {
+            *(gptr<f32x2>)(op + e) =
+                f32x2{static_cast<float>(res[v * N]), static_cast<float>(res[v * N + 1])};
+          } else {
+            if (e < count) op[e] = static_cast<float>(res[v * N]);
+            if (e + 1 < count) op[e + 1] = static_cast<float>(res[v * N + 1]);
+          }
+        }
+      }
+    } else {
+      const gptr<double> op = to_global_mut<double>(out_raw) + td.start;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const int e = (v * LANES + li) * N;
+#pragma unroll
+        for (int j = 0; j < N; j += 2) {
+          if (VEC && (FULL || e + j + 2 <= count)) {
+            *(gptr<f64x2>)(op + e + j) = f64x2{res[v * N + j], res[v * N + j + 1]};
+          } else {
+            if (e + j < count) op[e + j] = res[v * N + j];
+            if (e + j + 1 < count) op[e + j + 1] = res[v * N + j + 1];
+          }
+        }
+      }
+    }
+    const uint64_t ba = __ballot(bad_acc);
+    const uint64_t br = __ballot(bad_res);
+    if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+      atomicOr(a.flag, (ba ? FEDAVG_FLAG_ACC_NAN : 0u) | (br ? FEDAVG_FLAG_RESULT_NAN : 0u));
+    }
+  }
+}
+
+template <typename T, int OUT, int SPLIT, bool VEC>
+__global__ __launch_bounds__(kThreads) void fedavg_tile_kernel(KArgs a) {
+  __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
+  const TileDesc td = load_tile(a.tiles, a.tile_begin + blockIdx.x);
+  constexpr int TILE = kThreads / SPLIT * kAE;
+  if (td.count == TILE) {
+    tile_body<T, OUT, SPLIT, VEC, true>(a, td, lds);
+  } else {
+    tile_body<T, OUT, SPLIT, VEC, false>(a, td, lds);
+  }
+}
+
+// Diagnostic: per-client "holds a NaN" flags (error path only, fed_avg_algorithm.py:35).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void nan_scan_kernel(const TileDesc* tiles,
+                                                           const void* const* cptrs_tk,
+                                                           int32_t K, int32_t* bad) {
+  const TileDesc td = load_tile(tiles, blockIdx.x);
+  const int k = blockIdx.y;
+  const uint64_t raw = to_const<uint64_t>(cptrs_tk)[static_cast<int64_t>(td.seg) * K + k];
+  if (raw == 0) return;
+  const gptr<const T> p = to_global<T>(reinterpret_cast<const void*>(raw)) + td.start;
+  bool b = false;
+  for (int i = threadIdx.x; i < td.count; i += kThreads) {
+    const double x = load_g<T>(p, i);
+    b |= (x != x);
+  }
+  if (__ballot(b) != 0ull && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned*>(bad + k), 1u);
+}
+
+// Bandwidth probes (the measured HBM ceiling next to the roofline): mode 0 = float4 copy,
+// mode 1 = float4 read-only stream (xor-folded into one word per workgroup).
+__global__ __launch_bounds__(kThreads) void bw_copy_kernel(const float4* __restrict__ src,
+                                                          float4* __restrict__ dst, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+    dst[i] = src[i];
+  }
+}
+__global__ __launch_bounds__(kThreads) void bw_read_kernel(const float4* __restrict__ src,
+                                                          uint32_t* __restrict__ dst, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  uint32_t x = 0;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    x ^= __float_as_uint(a.x) ^ __float_as_uint(a.y) ^ __float_as_uint(a.z) ^ __float_as_uint(a.w);
+    x ^= __float_as_uint(b.x) ^ __float_as_uint(b.y) ^ __float_as_uint(b.z) ^ __float_as_uint(b.w);
+    x ^= __float_as_uint(c.x) ^ __float_as_uint(c.y) ^ __float_as_uint(c.z) ^ __float_as_uint(c.w);
+    x ^= __float_as_uint(d.x) ^ __float_as_uint(d.y) ^ __float_as_uint(d.z) ^ __float_as_uint(d.w);
+  }
+  for (; i < n; i += stride) {
+    const float4 a = src[i];
+    x ^= __float_as_uint(a.x) ^ __float_as_uint(a.y) ^ __float_as_uint(a.z) ^ __float_as_uint(a.w);
+  }
+  if (x == 0x9e3779b9u) dst[blockIdx.x] = x;  // practically never taken; keeps loads live
+}
+
+}  // namespace
+
+// =======================================================================================
+// host side
+// =======================================================================================
+struct fedavg_ctx {
+  int device = 0;
+  int T = 0;
+  std::vector<int64_t> seg_numel;
+  std::vector<int64_t> seg_acc_off;
+  int64_t acc_numel = 0;
+  double* acc = nullptr;
+  bool owns_acc = false;
+
+  // tiles for SPLIT=1 and SPLIT=4
+  std::vector<TileDesc> tiles1, tiles4;
+  TileDesc* d_tiles1 = nullptr;
+  TileDesc* d_tiles4 = nullptr;
+  SegDesc* d_segs = nullptr;
+  uint32_t* d_flag = nullptr;
+  uint32_t* h_flag = nullptr;  // pinned
+
+  // accumulated state (host mirror)
+  std::vector<double> wsum;     // per-segment total weight (fed_avg_algorithm.py:59-62)
+  std::vector<int32_t> valid;   // accumulator holds data for the segment
+
+  // staging ring for per-call tables
+  static constexpr int kSlots = 4;
+  struct Slot {
+    char* host = nullptr;  // pinned
+    char* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool used = false;
+  } slots[kSlots];
+  int next_slot = 0;
+
+  int split_policy = 1;  // 1 exact client order (default), 0 auto, 2 always split
+  // profiling
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+  std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int32_t elem_size(int32_t dt) {
+  switch (dt) {
+    case FEDAVG_F32: return 4;
+    case FEDAVG_F16: return 2;
+    case FEDAVG_BF16: return 2;
+    case FEDAVG_F64: return 8;
+    default: return 0;
+  }
+}
+
+void build_tiles(const std::vector<int64_t>& numel, int tile, std::vector<TileDesc>& out) {
+  out.clear();
+  for (size_t t = 0; t < numel.size(); ++t) {
+    for (int64_t s = 0; s < numel[t]; s += tile) {
+      TileDesc d;
+      d.seg = static_cast<int32_t>(t);
+      d.count = static_cast<int32_t>(std::min<int64_t>(tile, numel[t] - s));
+      d.start = s;
+      out.push_back(d);
+    }
+  }
+}
+
+hipEvent_t take_event(fedavg_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Staged per-call tables, laid out in one blob.
+struct Staged {
+  CallTables tab;
+  int32_t Kmax = 0;
+  int32_t stride = 1;    // row stride of the [T][K] tables
+  bool aligned = true;   // every client/out pointer is 16-byte aligned
+  std::vector<int32_t> kseg;
+};
+
+// Build segment-major compacted tables in a pinned slot and enqueue their H2D copy.
+int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptrs,
+                     const double* weights, int32_t K, void* const* out_ptrs,
+                     const double* wtot, const int32_t* acc_in, Staged& st) {
+  const int T = c->T;
+  const int Kr = std::max(K, 1);
+  const size_t off_ptr = 0;
+  const size_t off_w = align_up(off_ptr + sizeof(void*) * T * Kr, 16);
+  const size_t off_kseg = align_up(off_w + sizeof(double) * T * Kr, 16);
+  const size_t off_accin = align_up(off_kseg + sizeof(int32_t) * T, 16);
+  const size_t off_outs = align_up(off_accin + sizeof(int32_t) * T, 16);
+  const size_t off_wtot = align_up(off_outs + sizeof(void*) * T, 16);
+  const size_t bytes = align_up(off_wtot + sizeof(double) * T, 256);
+
+  fedavg_ctx::Slot& sl = c->slots[c->next_slot];
+  c->next_slot = (c->next_slot + 1) % fedavg_ctx::kSlots;
+  if (sl.used) FEDAVG_HIP_TRY(hipEventSynchronize(sl.done));  // its previous copy finished
+  if (sl.cap < bytes) {
+    if (sl.host) FEDAVG_HIP_TRY(hipHostFree(sl.host));
+    if (sl.dev) {
+      FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // a kernel may still read the old table
+      FEDAVG_HIP_TRY(hipFree(sl.dev));
+    }
+    const size_t cap = std::max<size_t>(bytes * 2, 64 * 1024);
+    FEDAVG_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sl.host), cap, hipHostMallocDefault));
+    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.dev), cap));
+    sl.cap = cap;
+    if (!sl.done) FEDAVG_HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  }
+  char* h = sl.host;
+  const void** hp = reinterpret_cast<const void**>(h + off_ptr);
+  double* hw = reinterpret_cast<double*>(h + off_w);
+  int32_t* hk = reinterpret_cast<int32_t*>(h + off_kseg);
+  int32_t* ha = reinterpret_cast<int32_t*>(h + off_accin);
+  void** ho = reinterpret_cast<void**>(h + off_outs);
+  double* hwt = reinterpret_cast<double*>(h + off_wtot);
+
+  st.kseg.assign(T, 0);
+  st.stride = Kr;
+  st.aligned = true;
+  st.Kmax = 0;
+  for (int t = 0; t < T; ++t) {
+    int n = 0;
+    for (int k = 0; k < K; ++k) {
+      const void* p = client_ptrs[static_cast<int64_t>(k) * T + t];
+      if (p == nullptr) continue;
+      if (reinterpret_cast<uintptr_t>(p) % 16 != 0) st.aligned = false;
+      hp[static_cast<int64_t>(t) * Kr + n] = p;
+      hw[static_cast<int64_t>(t) * Kr + n] = weights[static_cast<int64_t>(k) * T + t];
+      ++n;
+    }
+    hk[t] = n;
+    st.kseg[t] = n;
+    st.Kmax = std::max(st.Kmax, n);
+    ha[t] = acc_in ? acc_in[t] : 0;
+    ho[t] = out_ptrs ? out_ptrs[t] : nullptr;
+    if (out_ptrs && reinterpret_cast<uintptr_t>(out_ptrs[t]) % 16 != 0) st.aligned = false;
+    hwt[t] = wtot ? wtot[t] : 1.0;
+  }
+  FEDAVG_HIP_TRY(hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, s));
+  FEDAVG_HIP_TRY(hipEventRecord(sl.done, s));
+  sl.used = true;
+
+  char* d = sl.dev;
+  st.tab.cptrs = reinterpret_cast<const void* const*>(d + off_ptr);
+  st.tab.w = reinterpret_cast<const double*>(d + off_w);
+  st.tab.kseg = reinterpret_cast<const int32_t*>(d + off_kseg);
+  st.tab.acc_in = reinterpret_cast<const int32_t*>(d + off_accin);
+  st.tab.outs = reinterpret_cast<void* const*>(d + off_outs);
+  st.tab.wtot = reinterpret_cast<const double*>(d + off_wtot);
+  return FEDAVG_OK;
+}
+
+template <typename T, int OUT>
+hipError_t launch_typed(const KArgs& a, int split, bool vec, int nblocks, hipStream_t s) {
+  if (split == 4) {
+    if (vec) hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 4, true>), dim3(nblocks), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 4, false>), dim3(nblocks), dim3(kThreads), 0, s, a);
+  } else {
+    if (vec) hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, true>), dim3(nblocks), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, false>), dim3(nblocks), dim3(kThreads), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+template <int OUT>
+hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int nblocks, hipStream_t s) {
+  switch (in_dtype) {
+    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, nblocks, s);
+    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, nblocks, s);
+    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, nblocks, s);
+    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, nblocks, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int choose_split(const fedavg_ctx* c, int kmax) {
+  if (c->split_policy == 1) return 1;
+  if (c->split_policy == 2) return kmax >= 4 ? 4 : 1;
+  // auto: the exact-order kernel unless the tile grid cannot fill 256 CUs and there are
+  // enough clients per tile to keep four waves busy
+  if (static_cast<int64_t>(c->tiles1.size()) < 512 && kmax >= 16) return 4;
+  return 1;
+}
+
+// Launch the main kernel over tiles [tb, te) of the split-specific tile table.
+int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_dtype, int out_kind,
+                    int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1) {
+  KArgs a;
+  a.segs = c->d_segs;
+  a.tab = st.tab;
+  a.acc = c->acc;
+  a.flag = c->d_flag;
+  a.K = st.stride;
+  a.zero_init = zero_init;
+  int tb = 0, te = 0;
+  if (split == 4) {
+    // whole-layout launches only (tile ranges are defined on the SPLIT=1 table)
+    a.tiles = c->d_tiles4;
+    tb = 0;
+    te = static_cast<int>(c->tiles4.size());
+  } else {
+    a.tiles = c->d_tiles1;
+    tb = tb_split1;
+    te = te_split1;
+  }
+  a.tile_begin = tb;
+  const int nblocks = te - tb;
+  if (nblocks <= 0) return FEDAVG_OK;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->prof) {
+    e0 = take_event(c);
+    e1 = take_event(c);
+    if (!e0 || !e1) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
+    FEDAVG_HIP_TRY(hipEventRecord(e0, s));
+  }
+  hipError_t err = hipSuccess;
+  switch (out_kind) {
+    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, nblocks, s); break;
+    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, nblocks, s); break;
+    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, nblocks, s); break;
+    default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
+  }
+  if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
+  if (c->prof) {
+    FEDAVG_HIP_TRY(hipEventRecord(e1, s));
+    c->prof_events.emplace_back(e0, e1);
+  }
+  return FEDAVG_OK;
+}
+
+}  // namespace
+
+// =======================================================================================
+// exported C ABI (include/fedavg_hip.h)
+// =======================================================================================
+namespace {
+
+int32_t check_ctx(const fedavg_ctx* c) {
+  if (c == nullptr) return fail(FEDAVG_ERR_INVALID, "null context");
+  return FEDAVG_OK;
+}
+
+int32_t check_clients(const fedavg_ctx* c, const void* const* client_ptrs, const double* weights,
+                      int32_t K, int32_t in_dtype) {
+  if (K < 0) return fail(FEDAVG_ERR_INVALID, "num_clients < 0");
+  if (K > 0 && (client_ptrs == nullptr || weights == nullptr))
+    return fail(FEDAVG_ERR_INVALID, "null client table or weights");
+  if (K > 0 && elem_size(in_dtype) == 0) return fail(FEDAVG_ERR_INVALID, "bad input dtype");
+  (void)c;
+  return FEDAVG_OK;
+}
+
+int out_kind_of(int32_t out_dtype) {
+  if (out_dtype == FEDAVG_F32) return OUT_F32;
+  if (out_dtype == FEDAVG_F64) return OUT_F64;
+  return -1;
+}
+
+#define FEDAVG_RET(expr)            \
+  do {                              \
+    int32_t r_ = (expr);            \
+    if (r_ != FEDAVG_OK) return r_; \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int32_t fedavg_abi_version(void) { return FEDAVG_ABI_VERSION; }
+
+const char* fedavg_last_error(void) { return g_last_error.c_str(); }
+
+int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_numel,
+                          int32_t num_segments, void* accumulator) {
+  if (out == nullptr) return fail(FEDAVG_ERR_INVALID, "null out");
+  *out = nullptr;
+  if (num_segments <= 0 || seg_numel == nullptr) return fail(FEDAVG_ERR_INVALID, "no segments");
+  for (int t = 0; t < num_segments; ++t) {
+    if (seg_numel[t] <= 0) return fail(FEDAVG_ERR_INVALID, "segment with no elements");
+    if (seg_numel[t] > (int64_t(1) << 40)) return fail(FEDAVG_ERR_INVALID, "segment too large");
+  }
+  if (reinterpret_cast<uintptr_t>(accumulator) % 16 != 0)
+    return fail(FEDAVG_ERR_INVALID, "accumulator must be 16-byte aligned");
+  FEDAVG_HIP_TRY(hipSetDevice(device));
+  fedavg_ctx* c = new fedavg_ctx();
+  c->device = device;
+  c->T = num_segments;
+  c->seg_numel.assign(seg_numel, seg_numel + num_segments);
+  c->seg_acc_off.resize(num_segments);
+  int64_t off = 0;
+  for (int t = 0; t < num_segments; ++t) {
+    c->seg_acc_off[t] = off;
+    off += static_cast<int64_t>(align_up(static_cast<size_t>(seg_numel[t]), 2));
+  }
+  c->acc_numel = off;
+  c->wsum.assign(num_segments, 0.0);
+  c->valid.assign(num_segments, 0);
+  build_tiles(c->seg_numel, kTile1, c->tiles1);
+  build_tiles(c->seg_numel, kTile4, c->tiles4);
+  if (c->tiles1.size() > static_cast<size_t>(INT32_MAX / 2)) {
+    delete c;
+    return fail(FEDAVG_ERR_INVALID, "layout too large");
+  }
+  std::vector<SegDesc> segs(num_segments);
+  for (int t = 0; t < num_segments; ++t) segs[t] = SegDesc{c->seg_acc_off[t], c->seg_numel[t]};
+
+  auto cleanup = [&](hipError_t e, const char* what) {
+    fedavg_ctx_destroy(c);
+    return fail(FEDAVG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_tiles1), sizeof(TileDesc) * c->tiles1.size())) != hipSuccess)
+    return cleanup(e, "hipMalloc tiles1");
+  if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_tiles4), sizeof(TileDesc) * c->tiles4.size())) != hipSuccess)
+    return cleanup(e, "hipMalloc tiles4");
+  if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_segs), sizeof(SegDesc) * segs.size())) != hipSuccess)
+    return cleanup(e, "hipMalloc segs");
+  if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_flag), sizeof(uint32_t) * 4)) != hipSuccess)
+    return cleanup(e, "hipMalloc flag");
+  if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_flag), sizeof(uint32_t) * 4, hipHostMallocDefault)) != hipSuccess)
+    return cleanup(e, "hipHostMalloc flag");
+  if ((e = hipMemcpy(c->d_tiles1, c->tiles1.data(), sizeof(TileDesc) * c->tiles1.size(), hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "hipMemcpy tiles1");
+  if ((e = hipMemcpy(c->d_tiles4, c->tiles4.data(), sizeof(TileDesc) * c->tiles4.size(), hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "hipMemcpy tiles4");
+  if ((e = hipMemcpy(c->d_segs, segs.data(), sizeof(SegDesc) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "hipMemcpy segs");
+  if ((e = hipMemset(c->d_flag, 0, sizeof(uint32_t) * 4)) != hipSuccess) return cleanup(e, "hipMemset flag");
+  if (accumulator != nullptr) {
+    c->acc = static_cast<double*>(accumulator);
+    c->owns_acc = false;
+  } else {
+    if ((e = hipMalloc(reinterpret_cast<void**>(&c->acc), sizeof(double) * c->acc_numel)) != hipSuccess)
+      return cleanup(e, "hipMalloc accumulator");
+    c->owns_acc = true;
+    if ((e = hipMemset(c->acc, 0, sizeof(double) * c->acc_numel)) != hipSuccess)
+      return cleanup(e, "hipMemset accumulator");
+  }
+  *out = c;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
+  if (c == nullptr) return FEDAVG_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  for (auto& sl : c->slots) {
+    if (sl.host) (void)hipHostFree(sl.host);
+    if (sl.dev) (void)hipFree(sl.dev);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  for (auto& pr : c->prof_events) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->d_tiles1) (void)hipFree(c->d_tiles1);
+  if (c->d_tiles4) (void)hipFree(c->d_tiles4);
+  if (c->d_segs) (void)hipFree(c->d_segs);
+  if (c->d_flag) (void)hipFree(c->d_flag);
+  if (c->h_flag) (void)hipHostFree(c->h_flag);
+  if (c->owns_acc && c->acc) (void)hipFree(c->acc);
+  delete c;
+  return FEDAVG_OK;
+}
+
+int64_t fedavg_acc_numel(const fedavg_ctx* c) { return c ? c->acc_numel : -1; }
+
+int64_t fedavg_segment_offset(const fedavg_ctx* c, int32_t seg) {
+  if (!c || seg < 0 || seg >= c->T) return -1;
+  return c->seg_acc_off[seg];
+}
+
+void* fedavg_accumulator(const fedavg_ctx* c) { return c ? c->acc : nullptr; }
+
+int32_t fedavg_set_split_policy(fedavg_ctx* c, int32_t policy) {
+  FEDAVG_RET(check_ctx(c));
+  if (policy < 0 || policy > 2) return fail(FEDAVG_ERR_INVALID, "split policy must be 0, 1 or 2");
+  c->split_policy = policy;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_reset(fedavg_ctx* c, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
+  std::fill(c->valid.begin(), c->valid.end(), 0);
+  FEDAVG_HIP_TRY(hipMemsetAsync(c->d_flag, 0, sizeof(uint32_t) * 4, static_cast<hipStream_t>(stream)));
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_total_weights(const fedavg_ctx* c, double* out) {
+  FEDAVG_RET(check_ctx(c));
+  if (!out) return fail(FEDAVG_ERR_INVALID, "null out");
+  for (int t = 0; t < c->T; ++t) out[t] = c->wsum[t];
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_accumulate(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                          const double* weights, int32_t K, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  if (K == 0) return FEDAVG_OK;
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, client_ptrs, weights, K, nullptr, nullptr, c->valid.data(), st));
+  const int split = choose_split(c, st.Kmax);
+  FEDAVG_RET(launch_main(c, s, st, in_dtype, OUT_ACC, split, 0, 0, static_cast<int32_t>(c->tiles1.size())));
+  // host mirror: total weights in arrival order (fed_avg_algorithm.py:59-62)
+  for (int k = 0; k < K; ++k)
+    for (int t = 0; t < c->T; ++t)
+      if (client_ptrs[static_cast<int64_t>(k) * c->T + t] != nullptr) {
+        c->wsum[t] += weights[static_cast<int64_t>(k) * c->T + t];
+        c->valid[t] = 1;
+      }
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_aggregate(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                         const double* weights, int32_t K, void* const* out_ptrs, int32_t out_dtype,
+                         void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (out_ptrs == nullptr) return fail(FEDAVG_ERR_INVALID, "null out table");
+  for (int t = 0; t < c->T; ++t)
+    if (out_ptrs[t] == nullptr) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+  // totals including this last wave, in arrival order
+  std::vector<double> wtot(c->wsum);
+  std::vector<int32_t> will_have(c->valid);
+  for (int k = 0; k < K; ++k)
+    for (int t = 0; t < c->T; ++t)
+      if (client_ptrs[static_cast<int64_t>(k) * c->T + t] != nullptr) {
+        wtot[t] += weights[static_cast<int64_t>(k) * c->T + t];
+        will_have[t] = 1;
+      }
+  for (int t = 0; t < c->T; ++t)
+    if (!will_have[t])
+      return fail(FEDAVG_ERR_STATE, "segment " + std::to_string(t) +
+                                        " has no accumulated data (fed_avg_algorithm.py:88)");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, K > 0 ? client_ptrs : nullptr, weights, K, out_ptrs, wtot.data(),
+                          c->valid.data(), st));
+  const int split = choose_split(c, st.Kmax);
+  FEDAVG_RET(launch_main(c, s, st, K > 0 ? in_dtype : FEDAVG_F32, ok, split, 0, 0,
+                         static_cast<int32_t>(c->tiles1.size())));
+  // _aggregate_parameter resets the accumulator (fed_avg_algorithm.py:90,98)
+  std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
+  std::fill(c->valid.begin(), c->valid.end(), 0);
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_weighted_avg(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                            const double* ratios, int32_t K, void* const* out_ptrs, int32_t out_dtype,
+                            void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_RET(check_clients(c, client_ptrs, ratios, K, in_dtype));
+  if (K == 0) return fail(FEDAVG_ERR_STATE, "weighted_avg of no clients (aggregation_algorithm.py:57)");
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (out_ptrs == nullptr) return fail(FEDAVG_ERR_INVALID, "null out table");
+  for (int t = 0; t < c->T; ++t) {
+    if (out_ptrs[t] == nullptr) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+    bool any = false;
+    for (int k = 0; k < K && !any; ++k) any = client_ptrs[static_cast<int64_t>(k) * c->T + t] != nullptr;
+    if (!any) return fail(FEDAVG_ERR_STATE, "segment " + std::to_string(t) + " has no client data");
+  }
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::vector<int32_t> no_acc(c->T, 0);
+  std::vector<double> ones(c->T, 1.0);  // x / 1.0 == x exactly: no division on this path
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, client_ptrs, ratios, K, out_ptrs, ones.data(), no_acc.data(), st));
+  const int split = choose_split(c, st.Kmax);
+  return launch_main(c, s, st, in_dtype, ok, split, 0, 0, static_cast<int32_t>(c->tiles1.size()));
+}
+
+int32_t fedavg_num_tiles(const fedavg_ctx* c) {
+  if (!c) return -1;
+  return static_cast<int32_t>(c->tiles1.size());
+}
+
+int32_t fedavg_tile_range(const fedavg_ctx* c, int32_t tb, int32_t te, int64_t* acc_begin, int64_t* acc_end) {
+  FEDAVG_RET(check_ctx(c));
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (te < 0) te = n;
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  if (!acc_begin || !acc_end) return fail(FEDAVG_ERR_INVALID, "null out");
+  if (tb == te) {
+    *acc_begin = *acc_end = (tb < n) ? c->seg_acc_off[c->tiles1[tb].seg] + c->tiles1[tb].start : c->acc_numel;
+    return FEDAVG_OK;
+  }
+  const TileDesc& f = c->tiles1[tb];
+  const TileDesc& l = c->tiles1[te - 1];
+  *acc_begin = c->seg_acc_off[f.seg] + f.start;
+  // include the segment's alignment padding when the range ends a segment
+  const int64_t end = c->seg_acc_off[l.seg] + l.start + l.count;
+  *acc_end = (l.start + l.count == c->seg_numel[l.seg])
+                 ? ((l.seg + 1 < c->T) ? c->seg_acc_off[l.seg + 1] : c->acc_numel)
+                 : end;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_partial(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                       const double* weights, int32_t K, int32_t zero_init, int32_t tb, int32_t te,
+                       void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (te < 0) te = n;
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  if (!zero_init && K == 0) return FEDAVG_OK;
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, K > 0 ? client_ptrs : nullptr, weights, K, nullptr, nullptr,
+                          c->valid.data(), st));
+  // tile ranges are defined on the 2048-element tiles: the exact-order kernel
+  return launch_main(c, s, st, K > 0 ? in_dtype : FEDAVG_F32, OUT_ACC, 1, zero_init ? 1 : 0, tb, te);
+}
+
+int32_t fedavg_set_accumulated(fedavg_ctx* c, const double* total_weights) {
+  FEDAVG_RET(check_ctx(c));
+  if (!total_weights) return fail(FEDAVG_ERR_INVALID, "null total weights");
+  for (int t = 0; t < c->T; ++t) {
+    c->wsum[t] = total_weights[t];
+    c->valid[t] = 1;
+  }
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_finalize_range(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, int32_t tb,
+                              int32_t te, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (out_ptrs == nullptr) return fail(FEDAVG_ERR_INVALID, "null out table");
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (te < 0) te = n;
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  for (int t = 0; t < c->T; ++t) {
+    if (!c->valid[t]) return fail(FEDAVG_ERR_STATE, "segment " + std::to_string(t) + " not accumulated");
+    if (out_ptrs[t] == nullptr) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+  }
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, nullptr, nullptr, 0, out_ptrs, c->wsum.data(), c->valid.data(), st));
+  return launch_main(c, s, st, FEDAVG_F32, ok, 1, 0, tb, te);
+}
+
+int32_t fedavg_check(fedavg_ctx* c, void* stream, uint32_t* flags_out) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  FEDAVG_HIP_TRY(hipMemcpyAsync(c->h_flag, c->d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  FEDAVG_HIP_TRY(hipStreamSynchronize(s));
+  const uint32_t f = c->h_flag[0];
+  if (flags_out) *flags_out = f;
+  if (f & FEDAVG_FLAG_ACC_NAN) return fail(FEDAVG_ERR_NAN_ACCUM, "NaN in the accumulator");
+  if (f & FEDAVG_FLAG_RESULT_NAN) return fail(FEDAVG_ERR_NAN_RESULT, "NaN in the aggregated result");
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_find_nan_clients(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                                int32_t K, int32_t* out_bad, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  if (K <= 0 || !client_ptrs || !out_bad) return fail(FEDAVG_ERR_INVALID, "bad arguments");
+  if (elem_size(in_dtype) == 0) return fail(FEDAVG_ERR_INVALID, "bad input dtype");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // segment-major, uncompacted table (NULL = absent)
+  std::vector<const void*> tk(static_cast<size_t>(K) * c->T);
+  for (int k = 0; k < K; ++k)
+    for (int t = 0; t < c->T; ++t)
+      tk[static_cast<size_t>(t) * K + k] = client_ptrs[static_cast<size_t>(k) * c->T + t];
+  void* d_tab = nullptr;
+  int32_t* d_bad = nullptr;
+  FEDAVG_HIP_TRY(hipMalloc(&d_tab, sizeof(void*) * tk.size()));
+  FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_bad), sizeof(int32_t) * K));
+  hipError_t e = hipMemcpyAsync(d_tab, tk.data(), sizeof(void*) * tk.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, sizeof(int32_t) * K, s);
+  if (e == hipSuccess) {
+    dim3 grid(static_cast<unsigned>(c->tiles1.size()), static_cast<unsigned>(K));
+    const void* const* tab = static_cast<const void* const*>(d_tab);
+    switch (in_dtype) {
+      case FEDAVG_F32: hipLaunchKernelGGL(nan_scan_kernel<float>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
+      case FEDAVG_F16: hipLaunchKernelGGL(nan_scan_kernel<__half>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
+      case FEDAVG_BF16: hipLaunchKernelGGL(nan_scan_kernel<bf16_t>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
+      default: hipLaunchKernelGGL(nan_scan_kernel<double>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
+    }
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out_bad, d_bad, sizeof(int32_t) * K, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d_tab);
+  (void)hipFree(d_bad);
+  if (e != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("find_nan_clients: ") + hipGetErrorString(e));
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_prof_enable(fedavg_ctx* c, int32_t enable) {
+  FEDAVG_RET(check_ctx(c));
+  c->prof = enable != 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_prof_collect(fedavg_ctx* c, double* total_ms, int32_t* launches) {
+  FEDAVG_RET(check_ctx(c));
+  double sum = 0.0;
+  for (auto& pr : c->prof_events) {
+    FEDAVG_HIP_TRY(hipEventSynchronize(pr.second));
+    float ms = 0.f;
+    FEDAVG_HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    sum += ms;
+  }
+  if (total_ms) *total_ms = sum;
+  if (launches) *launches = static_cast<int32_t>(c->prof_events.size());
+  for (auto& pr : c->prof_events) {
+    c->event_pool.push_back(pr.first);
+    c->event_pool.push_back(pr.second);
+  }
+  c->prof_events.clear();
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_bw_probe(const void* src, int64_t bytes, void* dst, int32_t mode, void* stream) {
+  if (!src || !dst || bytes <= 0 || bytes % 16 != 0) return fail(FEDAVG_ERR_INVALID, "bad probe args");
+  if (reinterpret_cast<uintptr_t>(src) % 16 || reinterpret_cast<uintptr_t>(dst) % 16)
+    return fail(FEDAVG_ERR_INVALID, "probe buffers must be 16-byte aligned");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = bytes / 16;
+  const int blocks = 256 * 8;
+  if (mode == 0) {
+    hipLaunchKernelGGL(bw_copy_kernel, dim3(blocks), dim3(kThreads), 0, s, static_cast<const float4*>(src),
+                       static_cast<float4*>(dst), n);
+  } else {
+    hipLaunchKernelGGL(bw_read_kernel, dim3(blocks), dim3(kThreads), 0, s, static_cast<const float4*>(src),
+                       static_cast<uint32_t*>(dst), n);
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  return FEDAVG_OK;
+}
+
+}  // extern "C"

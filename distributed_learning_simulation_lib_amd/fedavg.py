@@ -1,0 +1,382 @@
+"""Host-side handle on the HIP FedAvg library: model layouts, client tables, error mapping.
+
+A ``ModelLayout`` is the ordered list of named tensors of a model — the keys of
+``ParameterMessage.parameter`` (reference ``simulation_lib/message.py:24-31``). A
+``FedAvgContext`` owns one native context (``include/fedavg_hip.h``) for one layout on one
+device: the fp64 accumulator the streaming path folds clients into
+(``fed_avg_algorithm.py:43-64``), the per-segment total weights, and the fused
+finalize/NaN checks (``fed_avg_algorithm.py:76-99``).
+
+Every method launches asynchronously on the current torch stream of the context's device
+(``torch.cuda.current_stream``); PyTorch is only the allocator and stream provider here. The
+arithmetic runs in the HIP kernels of ``csrc/fedavg_kernels.hip``; there is no CPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from collections.abc import Mapping, Sequence
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native
+
+DTYPE_CODES: dict[torch.dtype, int] = {
+    torch.float32: _native.F32,
+    torch.float16: _native.F16,
+    torch.bfloat16: _native.BF16,
+    torch.float64: _native.F64,
+}
+OUT_CODES: dict[torch.dtype, int] = {torch.float32: _native.F32, torch.float64: _native.F64}
+
+_PTR = ctypes.POINTER(ctypes.c_void_p)
+_DBL = ctypes.POINTER(ctypes.c_double)
+
+
+class NaNAggregationError(AssertionError):
+    """Raised where the reference's NaN assertions fire (fed_avg_algorithm.py:35,93,97).
+
+    Subclasses ``AssertionError`` so callers that expect the reference's ``assert`` keep
+    working. ``stage`` is ``"input"`` (:35), ``"accumulator"`` (:93) or ``"result"`` (:97).
+    """
+
+    def __init__(self, stage: str, message: str, bad_clients: Sequence[int] = ()) -> None:
+        super().__init__(message)
+        self.stage = stage
+        self.bad_clients = list(bad_clients)
+
+
+@dataclass(frozen=True)
+class ModelLayout:
+    """Names, shapes and element counts of a model's tensors, in dict order."""
+
+    names: tuple[str, ...]
+    shapes: tuple[tuple[int, ...], ...]
+
+    @classmethod
+    def from_parameters(cls, parameter: Mapping[str, torch.Tensor]) -> ModelLayout:
+        return cls(
+            names=tuple(parameter.keys()),
+            shapes=tuple(tuple(t.shape) for t in parameter.values()),
+        )
+
+    @classmethod
+    def flat(cls, numel: int, name: str = "bucket") -> ModelLayout:
+        return cls(names=(name,), shapes=((int(numel),),))
+
+    @property
+    def numels(self) -> list[int]:
+        return [int(np.prod(s, dtype=np.int64)) for s in self.shapes]
+
+    @property
+    def num_segments(self) -> int:
+        return len(self.names)
+
+    @property
+    def total_numel(self) -> int:
+        return sum(self.numels)
+
+    def padded_offsets(self, elem_bytes: int) -> tuple[list[int], int]:
+        """Element offsets of each tensor in a flat buffer whose segments start 16-B aligned."""
+        align = max(1, 16 // elem_bytes)
+        offs, pos = [], 0
+        for n in self.numels:
+            offs.append(pos)
+            pos += (n + align - 1) // align * align
+        return offs, pos
+
+
+def _stream_handle(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    try:
+        return DTYPE_CODES[dtype]
+    except KeyError:
+        raise TypeError(f"no HIP FedAvg kernel for input dtype {dtype}") from None
+
+
+def out_code(dtype: torch.dtype) -> int:
+    try:
+        return OUT_CODES[dtype]
+    except KeyError:
+        raise TypeError(f"aggregated output dtype must be float32 or float64, not {dtype}") from None
+
+
+class ClientTable:
+    """Row-major [num_clients][num_segments] device pointers + fp64 weights for one call.
+
+    ``None`` entries are absent tensors (skipped, never counted in the segment's total
+    weight). The tensors are kept alive by the table until the caller drops it.
+    """
+
+    def __init__(self, num_segments: int) -> None:
+        self.num_segments = num_segments
+        self._ptrs: list[int] = []
+        self._weights: list[float] = []
+        self._keep: list[torch.Tensor] = []
+        self.num_clients = 0
+
+    def add_client(self, tensors: Sequence[torch.Tensor | None], weights: Sequence[float]) -> None:
+        if len(tensors) != self.num_segments or len(weights) != self.num_segments:
+            raise ValueError("client row does not match the layout")
+        for t, w in zip(tensors, weights):
+            if t is None:
+                self._ptrs.append(0)
+                self._weights.append(0.0)
+            else:
+                self._ptrs.append(t.data_ptr())
+                self._weights.append(float(w))
+                self._keep.append(t)
+        self.num_clients += 1
+
+    def arrays(self) -> tuple[np.ndarray, np.ndarray]:
+        ptrs = np.asarray(self._ptrs, dtype=np.uint64) if self._ptrs else np.zeros(1, np.uint64)
+        ws = np.asarray(self._weights, dtype=np.float64) if self._weights else np.zeros(1, np.float64)
+        return ptrs, ws
+
+    def rows(self) -> list[list[int]]:
+        T = self.num_segments
+        return [self._ptrs[k * T : (k + 1) * T] for k in range(self.num_clients)]
+
+
+class FedAvgContext:
+    """One native FedAvg context: layout + device + fp64 accumulator."""
+
+    def __init__(
+        self,
+        layout: ModelLayout,
+        device: torch.device | str | int | None = None,
+        split_policy: int | None = None,
+    ) -> None:
+        self._lib = _native.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("the FedAvg HIP path runs on a GPU device")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.layout = layout
+        if layout.num_segments == 0 or min(layout.numels) <= 0:
+            raise ValueError("a native layout needs at least one tensor and no empty tensors")
+        numels = (ctypes.c_int64 * layout.num_segments)(*layout.numels)
+        # the accumulator is a torch tensor so collectives (RCCL) can run on it
+        acc_numel = self._padded_acc_numel(layout)
+        self.accumulator = torch.zeros(acc_numel, dtype=torch.float64, device=device)
+        handle = ctypes.c_void_p()
+        _native.check(
+            self._lib.fedavg_ctx_create(
+                ctypes.byref(handle),
+                device.index,
+                numels,
+                layout.num_segments,
+                ctypes.c_void_p(self.accumulator.data_ptr()),
+            )
+        )
+        self._h = handle
+        assert self._lib.fedavg_acc_numel(self._h) == acc_numel
+        if split_policy is not None:
+            _native.check(self._lib.fedavg_set_split_policy(self._h, split_policy))
+
+    @staticmethod
+    def _padded_acc_numel(layout: ModelLayout) -> int:
+        return layout.padded_offsets(8)[1]
+
+    # -- lifecycle -------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.fedavg_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self) -> None:  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- helpers ---------------------------------------------------------------------
+    @property
+    def stream(self) -> ctypes.c_void_p:
+        return _stream_handle(self.device)
+
+    def segment_offset(self, seg: int) -> int:
+        return int(self._lib.fedavg_segment_offset(self._h, seg))
+
+    @property
+    def num_tiles(self) -> int:
+        return int(self._lib.fedavg_num_tiles(self._h))
+
+    def tile_range(self, tile_begin: int, tile_end: int) -> tuple[int, int]:
+        b, e = ctypes.c_int64(), ctypes.c_int64()
+        _native.check(self._lib.fedavg_tile_range(self._h, tile_begin, tile_end, ctypes.byref(b), ctypes.byref(e)))
+        return b.value, e.value
+
+    def total_weights(self) -> list[float]:
+        out = (ctypes.c_double * self.layout.num_segments)()
+        _native.check(self._lib.fedavg_total_weights(self._h, out))
+        return list(out)
+
+    def _out_table(self, outs: Sequence[torch.Tensor], out_dtype: torch.dtype) -> ctypes.Array:
+        if len(outs) != self.layout.num_segments:
+            raise ValueError("one output tensor per segment is required")
+        for o, n in zip(outs, self.layout.numels):
+            if o.dtype != out_dtype or o.device != self.device or o.numel() != n or not o.is_contiguous():
+                raise ValueError("output tensors must be contiguous, on the context device, of the layout size")
+        return (ctypes.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
+
+    def _check_table(self, table: ClientTable, in_dtype: torch.dtype) -> None:
+        if table.num_segments != self.layout.num_segments:
+            raise ValueError("client table does not match the layout")
+        dtype_code(in_dtype)
+
+    # -- hot path --------------------------------------------------------------------
+    def accumulate(self, table: ClientTable, in_dtype: torch.dtype) -> None:
+        """Fold a wave of clients into the accumulator (fed_avg_algorithm.py:43-64)."""
+        self._check_table(table, in_dtype)
+        if table.num_clients == 0:
+            return
+        p, w = table.arrays()
+        _native.check(
+            self._lib.fedavg_accumulate(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), w.ctypes.data_as(_DBL),
+                table.num_clients, self.stream,
+            )
+        )
+
+    def aggregate(
+        self,
+        table: ClientTable | None,
+        in_dtype: torch.dtype,
+        outs: Sequence[torch.Tensor],
+        out_dtype: torch.dtype,
+    ) -> None:
+        """Fold the last wave (optional) then out = acc / total_weight (fed_avg_algorithm.py:76-99)."""
+        n = 0 if table is None else table.num_clients
+        if table is not None:
+            self._check_table(table, in_dtype)
+            p, w = table.arrays()
+        else:
+            p, w = np.zeros(1, np.uint64), np.zeros(1, np.float64)
+        ot = self._out_table(outs, out_dtype)
+        _native.check(
+            self._lib.fedavg_aggregate(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype) if n else _native.F32,
+                w.ctypes.data_as(_DBL), n, ot, out_code(out_dtype), self.stream,
+            )
+        )
+
+    def weighted_avg(
+        self, table: ClientTable, in_dtype: torch.dtype, outs: Sequence[torch.Tensor], out_dtype: torch.dtype
+    ) -> None:
+        """out = sum_k ratio_k * x_k in fp64, table weights are the ratios (aggregation_algorithm.py:51-76)."""
+        self._check_table(table, in_dtype)
+        p, w = table.arrays()
+        ot = self._out_table(outs, out_dtype)
+        _native.check(
+            self._lib.fedavg_weighted_avg(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), w.ctypes.data_as(_DBL),
+                table.num_clients, ot, out_code(out_dtype), self.stream,
+            )
+        )
+
+    def partial(
+        self,
+        table: ClientTable | None,
+        in_dtype: torch.dtype,
+        zero_init: bool = True,
+        tile_begin: int = 0,
+        tile_end: int = -1,
+    ) -> None:
+        """acc[tiles] = (0 | acc) + sum_k w_k x_k (the shard step of the multi-GPU path)."""
+        n = 0 if table is None else table.num_clients
+        if table is not None:
+            self._check_table(table, in_dtype)
+            p, w = table.arrays()
+        else:
+            p, w = np.zeros(1, np.uint64), np.zeros(1, np.float64)
+        _native.check(
+            self._lib.fedavg_partial(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype) if n else _native.F32,
+                w.ctypes.data_as(_DBL), n, 1 if zero_init else 0, tile_begin, tile_end, self.stream,
+            )
+        )
+
+    def set_accumulated(self, total_weights: Sequence[float]) -> None:
+        tw = (ctypes.c_double * self.layout.num_segments)(*[float(x) for x in total_weights])
+        _native.check(self._lib.fedavg_set_accumulated(self._h, tw))
+
+    def finalize_range(
+        self, outs: Sequence[torch.Tensor], out_dtype: torch.dtype, tile_begin: int = 0, tile_end: int = -1
+    ) -> None:
+        ot = self._out_table(outs, out_dtype)
+        _native.check(
+            self._lib.fedavg_finalize_range(self._h, ot, out_code(out_dtype), tile_begin, tile_end, self.stream)
+        )
+
+    def reset(self) -> None:
+        _native.check(self._lib.fedavg_reset(self._h, self.stream))
+
+    # -- fault reporting ---------------------------------------------------------------
+    def flags(self) -> int:
+        """Synchronise the stream and return the latched NaN flag bits."""
+        f = ctypes.c_uint32()
+        st = self._lib.fedavg_check(self._h, self.stream, ctypes.byref(f))
+        if st not in (_native.OK, _native.ERR_NAN_ACCUM, _native.ERR_NAN_RESULT):
+            _native.check(st)
+        return int(f.value)
+
+    def find_nan_clients(self, table: ClientTable, in_dtype: torch.dtype) -> list[int]:
+        p, _ = table.arrays()
+        out = (ctypes.c_int32 * table.num_clients)()
+        _native.check(
+            self._lib.fedavg_find_nan_clients(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), table.num_clients, out, self.stream
+            )
+        )
+        return [i for i in range(table.num_clients) if out[i]]
+
+    def raise_on_nan(self, tables: Sequence[tuple[ClientTable, torch.dtype]] = ()) -> None:
+        """Map the latched flags onto the reference's assertions.
+
+        Input NaN (fed_avg_algorithm.py:35) and an accumulator NaN (:93) both leave the fp64
+        accumulator NaN; the client tables still held by the caller are scanned to tell them
+        apart and name the offending clients.
+        """
+        f = self.flags()
+        if f == 0:
+            return
+        # the flag is sticky until reset: clear it so the context stays usable
+        self.reset()
+        if f & _native.FLAG_ACC_NAN:
+            for table, dt in tables:
+                bad = self.find_nan_clients(table, dt)
+                if bad:
+                    raise NaNAggregationError("input", f"NaN in client update(s) at table rows {bad}", bad)
+            raise NaNAggregationError("accumulator", "NaN in the weighted sum (e.g. inf - inf)")
+        raise NaNAggregationError("result", "NaN after dividing by the total weight (e.g. 0 / 0)")
+
+    # -- measurement -------------------------------------------------------------------
+    def prof_enable(self, on: bool = True) -> None:
+        _native.check(self._lib.fedavg_prof_enable(self._h, 1 if on else 0))
+
+    def prof_collect(self) -> tuple[float, int]:
+        ms, n = ctypes.c_double(), ctypes.c_int32()
+        _native.check(self._lib.fedavg_prof_collect(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+def bw_probe(src: torch.Tensor, dst: torch.Tensor, mode: int) -> None:
+    """HBM ceiling probe: mode 0 copies src->dst (16-B lanes), mode 1 only reads src."""
+    lib = _native.load()
+    nbytes = src.numel() * src.element_size()
+    _native.check(
+        lib.fedavg_bw_probe(
+            ctypes.c_void_p(src.data_ptr()), nbytes, ctypes.c_void_p(dst.data_ptr()), mode,
+            _stream_handle(src.device),
+        )
+    )

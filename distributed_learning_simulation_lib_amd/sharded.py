@@ -1,0 +1,142 @@
+"""Clients sharded across the GPUs of a node, one RCCL reduce of the fp64 partials.
+
+The reference has no collectives: every client update goes to the one server process
+(SURVEY.md §5). When N × model bytes outgrows one GPU (BASELINE.json configs 3 and 5), the
+clients are partitioned over the ranks (one process per GPU, ``torch.distributed`` with the
+``nccl`` backend = RCCL over xGMI):
+
+    rank r:  S_r = sum_{k in shard r} w_k x_k           (fp64, HIP partial kernel)
+    root:    S   = sum_r S_r                            (RCCL reduce, chunked)
+    root:    out = S / W                                (HIP finalize kernel, per chunk)
+
+The partial is produced and reduced in chunks of tiles: the kernel for chunk c+1 runs on
+the compute stream while RCCL reduces chunk c on its own stream, and the root finalizes
+chunk c as soon as its reduce has landed. This is the only exchange step of the path.
+
+Numerics: each rank accumulates its clients in arrival order exactly like the single-GPU
+kernel; the cross-rank sum reorders fp64 additions, so results match the reference to fp64
+rounding (|Δ| ≤ 1e-12 relative; after an fp32 cast, identical in practice) instead of
+bit-for-bit. Total weights: integer weights sum exactly; float weights to fp64 rounding.
+
+``LocalReducer`` is the per-rank compute interface; ``HipLocalReducer`` is the product
+implementation. Tests on CPU (gloo) plug a plain torch reducer in its place to cover the
+chunking / collective / finalize logic without a GPU.
+"""
+
+from __future__ import annotations
+
+from collections.abc import Sequence
+from typing import Protocol
+
+import torch
+import torch.distributed as dist
+
+from .fedavg import ClientTable, FedAvgContext
+
+
+class LocalReducer(Protocol):
+    accumulator: torch.Tensor
+
+    @property
+    def num_tiles(self) -> int: ...
+
+    def tile_range(self, tile_begin: int, tile_end: int) -> tuple[int, int]: ...
+
+    def partial(self, tile_begin: int, tile_end: int) -> None: ...
+
+    def set_accumulated(self, total_weights: Sequence[float]) -> None: ...
+
+    def finalize_range(self, tile_begin: int, tile_end: int) -> None: ...
+
+    def fused(self) -> None: ...
+
+
+class HipLocalReducer:
+    """The shard's clients, reduced by the HIP kernels of one FedAvgContext."""
+
+    def __init__(
+        self,
+        ctx: FedAvgContext,
+        table: ClientTable | None,
+        in_dtype: torch.dtype,
+        outs: Sequence[torch.Tensor] | None,
+        out_dtype: torch.dtype,
+    ) -> None:
+        self.ctx = ctx
+        self.table = table
+        self.in_dtype = in_dtype
+        self.outs = outs
+        self.out_dtype = out_dtype
+        self.accumulator = ctx.accumulator
+
+    @property
+    def num_tiles(self) -> int:
+        return self.ctx.num_tiles
+
+    def tile_range(self, tile_begin: int, tile_end: int) -> tuple[int, int]:
+        return self.ctx.tile_range(tile_begin, tile_end)
+
+    def partial(self, tile_begin: int, tile_end: int) -> None:
+        self.ctx.partial(self.table, self.in_dtype, zero_init=True, tile_begin=tile_begin, tile_end=tile_end)
+
+    def set_accumulated(self, total_weights: Sequence[float]) -> None:
+        self.ctx.set_accumulated(total_weights)
+
+    def finalize_range(self, tile_begin: int, tile_end: int) -> None:
+        assert self.outs is not None
+        self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
+
+    def fused(self) -> None:
+        """Single-rank shortcut: fold + divide in one launch, no fp64 round trip."""
+        assert self.outs is not None
+        self.ctx.aggregate(self.table, self.in_dtype, self.outs, self.out_dtype)
+
+
+def chunk_bounds(num_tiles: int, chunks: int) -> list[tuple[int, int]]:
+    chunks = max(1, min(chunks, num_tiles))
+    edges = [round(i * num_tiles / chunks) for i in range(chunks + 1)]
+    return [(edges[i], edges[i + 1]) for i in range(chunks) if edges[i + 1] > edges[i]]
+
+
+def sharded_reduce(
+    reducer: LocalReducer,
+    local_total_weights: Sequence[float],
+    chunks: int = 4,
+    root: int = 0,
+    group: dist.ProcessGroup | None = None,
+    global_total_weights: Sequence[float] | None = None,
+) -> list[float]:
+    """One FedAvg reduce over every rank's shard; the result lands in the root's outputs.
+
+    ``local_total_weights`` are this rank's per-segment sums of client weights. When the
+    caller already knows the global totals (the dispatcher that assigned clients to ranks
+    knows every client's weight) it passes ``global_total_weights`` and no collective is
+    spent on them; otherwise they are all-reduced first. Returns the global totals. On a
+    one-rank world the fused single-launch kernel is used (no fp64 round trip).
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        reducer.fused()
+        return list(local_total_weights)
+    rank = dist.get_rank(group)
+    if global_total_weights is None:
+        totals = torch.tensor([float(w) for w in local_total_weights], dtype=torch.float64,
+                              device=reducer.accumulator.device)
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
+        global_total_weights = totals.tolist()
+    global_totals = [float(w) for w in global_total_weights]
+    bounds = chunk_bounds(reducer.num_tiles, chunks)
+    works = []
+    for tb, te in bounds:
+        reducer.partial(tb, te)
+        a, b = reducer.tile_range(tb, te)
+        works.append(
+            dist.reduce(reducer.accumulator[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        )
+    if rank == root:
+        reducer.set_accumulated(global_totals)
+    for (tb, te), w in zip(bounds, works):
+        w.wait()
+        if rank == root:
+            reducer.finalize_range(tb, te)
+    return global_totals

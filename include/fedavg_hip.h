@@ -1,0 +1,191 @@
+/*
+ * fedavg_hip.h — C ABI of the MI355X-native FedAvg aggregation path.
+ *
+ * This is the drop-in boundary for the server-side weighted FedAvg reduction of
+ * cyyever/distributed_learning_simulation_lib. Every entry point below replaces one
+ * piece of the reference's Python hot path (paths relative to the reference root):
+ *
+ *   fedavg_accumulate    <- FedAVGAlgorithm.process_worker_data / _accumulate_parameter
+ *                           simulation_lib/algorithm/fed_avg_algorithm.py:20-64
+ *   fedavg_aggregate     <- FedAVGAlgorithm._aggregate_parameter / _apply_total_weight
+ *                           simulation_lib/algorithm/fed_avg_algorithm.py:71-99
+ *   fedavg_weighted_avg  <- AggregationAlgorithm.weighted_avg (ratio path, accumulate=False)
+ *                           simulation_lib/algorithm/aggregation_algorithm.py:51-76
+ *   fedavg_partial       <- the per-shard half of _accumulate_parameter when clients are
+ *                           sharded across GPUs (fp64 partial sum, no division)
+ *   fedavg_check         <- the NaN assertions fed_avg_algorithm.py:35,93,97
+ *   fedavg_find_nan_clients <- which client tripped fed_avg_algorithm.py:35
+ *
+ * Conventions
+ *  - Plain C types only. Device pointers are `const void*` / `void*`; a stream is a
+ *    `hipStream_t` passed as `void*` (NULL = the legacy default stream).
+ *  - A "layout" is the ordered list of named tensors of one model (the keys of
+ *    ParameterMessage.parameter, message.py:24-31). Segment t has seg_numel[t] elements.
+ *  - A client table is row-major [num_clients][num_segments] of device pointers; a NULL
+ *    entry means "this client did not send this tensor" (it is skipped, exactly like a
+ *    missing key in the reference's per-name dictionaries, fed_avg_algorithm.py:56-62).
+ *  - Weights are fp64, [num_clients][num_segments] (the value _get_weight returns for
+ *    that (client, tensor), fed_avg_algorithm.py:66-69).
+ *  - Accumulation is fp64 in arrival order: acc = x0*w0, then acc = acc + xk*wk, with the
+ *    product and the sum each rounded (no FMA), exactly the reference's
+ *    `tmp = x.to(f64) * w; acc += tmp`. Results are bit-identical to the reference for the
+ *    single-GPU kernels.
+ *  - Every call is asynchronous on `stream`. Arithmetic faults (NaN) are latched in a
+ *    device flag and reported by fedavg_check(), which synchronises the stream.
+ *  - Return value: FEDAVG_OK (0) or a negative/positive status below; the text of the
+ *    last error of the calling thread is returned by fedavg_last_error().
+ *  - The library never frees caller memory. Client buffers must stay valid until the
+ *    call's stream work completes. One host thread per context.
+ */
+#ifndef FEDAVG_HIP_H
+#define FEDAVG_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FEDAVG_ABI_VERSION 1
+
+/* element types */
+enum fedavg_dtype {
+  FEDAVG_F32 = 0,
+  FEDAVG_F16 = 1,
+  FEDAVG_BF16 = 2,
+  FEDAVG_F64 = 3,
+};
+
+/* status codes */
+enum fedavg_status {
+  FEDAVG_OK = 0,
+  FEDAVG_ERR_NAN_INPUT = 1,    /* a client tensor holds NaN   (fed_avg_algorithm.py:35) */
+  FEDAVG_ERR_NAN_ACCUM = 2,    /* accumulator became NaN      (fed_avg_algorithm.py:93) */
+  FEDAVG_ERR_NAN_RESULT = 3,   /* acc / total_weight is NaN   (fed_avg_algorithm.py:97) */
+  FEDAVG_ERR_INVALID = 4,      /* bad argument / dtype / size */
+  FEDAVG_ERR_HIP = 5,          /* HIP runtime error */
+  FEDAVG_ERR_STATE = 6,        /* e.g. aggregate with nothing accumulated (:88 assert) */
+};
+
+/* flag bits latched by the kernels (read through fedavg_check) */
+#define FEDAVG_FLAG_ACC_NAN 0x1u
+#define FEDAVG_FLAG_RESULT_NAN 0x2u
+
+typedef struct fedavg_ctx fedavg_ctx;
+
+int32_t fedavg_abi_version(void);
+const char* fedavg_last_error(void);
+
+/*
+ * Create a context for one model layout on one device.
+ *  seg_numel[num_segments]: element count of each named tensor, in dict order.
+ *  accumulator: optional caller-owned fp64 device buffer of fedavg_acc_numel() elements
+ *               (e.g. a torch tensor, so a collective can run on it); NULL = the context
+ *               allocates its own.
+ * The fp64 accumulator uses a padded flat layout: segment t starts at
+ * fedavg_segment_offset(ctx, t) (a multiple of 2 elements = 16 bytes).
+ */
+int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_numel,
+                          int32_t num_segments, void* accumulator);
+int32_t fedavg_ctx_destroy(fedavg_ctx* ctx);
+int64_t fedavg_acc_numel(const fedavg_ctx* ctx);
+int64_t fedavg_segment_offset(const fedavg_ctx* ctx, int32_t seg);
+void* fedavg_accumulator(const fedavg_ctx* ctx);
+
+/* Summation-order policy:
+ *  1 = (default) the exact client-order kernel: bit-identical to the reference;
+ *  0 = auto: the LDS split-client kernel when the layout is too small to fill the chip
+ *      (< 512 tiles of 2048 elements) and a call carries >= 16 clients, else exact order;
+ *  2 = the split-client kernel whenever a call carries >= 4 clients.
+ * The split kernel reorders the fp64 sum (four wave partials combined in LDS). */
+int32_t fedavg_set_split_policy(fedavg_ctx* ctx, int32_t policy);
+
+/* Forget accumulated state and the NaN flag (AggregationAlgorithm.clear_worker_data,
+ * aggregation_algorithm.py:107-109). Asynchronous on stream. */
+int32_t fedavg_reset(fedavg_ctx* ctx, void* stream);
+
+/* Host-side per-segment total weight so far (fed_avg_algorithm.py:59-62). out[num_segments]. */
+int32_t fedavg_total_weights(const fedavg_ctx* ctx, double* out);
+
+/*
+ * Streaming accumulate of a wave of clients into the fp64 accumulator, in table order.
+ * Equivalent to calling _accumulate_parameter for every (client, tensor) of the wave in
+ * arrival order (fed_avg_algorithm.py:43-64). Per-segment total weights accumulate on the
+ * host in the same order.
+ */
+int32_t fedavg_accumulate(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                          const double* weights, int32_t num_clients, void* stream);
+
+/*
+ * Finish the round: optionally fold a last wave of clients (num_clients may be 0), then
+ * out[t] = acc[t] / total_weight[t] converted to out_dtype (FEDAVG_F32 or FEDAVG_F64),
+ * written through out_ptrs[num_segments] (device pointers). Resets the accumulator state
+ * (fed_avg_algorithm.py:88-99). The acc and result NaN checks are fused in the kernel.
+ * FEDAVG_ERR_STATE if nothing was ever accumulated for some segment (the :88 assert).
+ */
+int32_t fedavg_aggregate(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                         const double* weights, int32_t num_clients, void* const* out_ptrs,
+                         int32_t out_dtype, void* stream);
+
+/*
+ * Non-streaming ratio path (accumulate=False): out = sum_k ratio[k] * x_k in fp64, no
+ * division (aggregation_algorithm.py:51-76). `ratios` is [num_clients][num_segments];
+ * the caller computes ratios exactly like get_ratios (aggregation_algorithm.py:42-49).
+ * Does not touch the accumulator.
+ */
+int32_t fedavg_weighted_avg(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                            const double* ratios, int32_t num_clients, void* const* out_ptrs,
+                            int32_t out_dtype, void* stream);
+
+/*
+ * Multi-GPU shard step: acc[tiles in [tile_begin, tile_end)] = (acc_in ? acc : 0) +
+ * sum_k w_k x_k, fp64, written to the accumulator (no division). Used by the sharded
+ * driver that reduces the per-GPU partials with RCCL and then calls fedavg_aggregate
+ * with num_clients = 0 on the root. tile_end = -1 means "all tiles". zero_init != 0 starts
+ * every segment at +0.0 (so a shard without clients contributes exact zeros).
+ */
+int32_t fedavg_partial(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                       const double* weights, int32_t num_clients, int32_t zero_init,
+                       int32_t tile_begin, int32_t tile_end, void* stream);
+/* Number of tiles and the accumulator element range [*acc_begin, *acc_end) of tiles
+ * [tile_begin, tile_end), for chunking a collective over the partial. */
+int32_t fedavg_num_tiles(const fedavg_ctx* ctx);
+int32_t fedavg_tile_range(const fedavg_ctx* ctx, int32_t tile_begin, int32_t tile_end,
+                          int64_t* acc_begin, int64_t* acc_end);
+/* Declare that segments' accumulators hold data and add host totals (after an external
+ * collective summed partials into the accumulator): total_weights[num_segments]. */
+int32_t fedavg_set_accumulated(fedavg_ctx* ctx, const double* total_weights);
+/* Finalize only tiles [tile_begin, tile_end) of the accumulator into out_ptrs (used to
+ * pipeline finalize behind a chunked collective). Does not reset state. */
+int32_t fedavg_finalize_range(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dtype,
+                              int32_t tile_begin, int32_t tile_end, void* stream);
+
+/*
+ * Synchronise `stream` and report the NaN flag: FEDAVG_OK, FEDAVG_ERR_NAN_ACCUM or
+ * FEDAVG_ERR_NAN_RESULT. *flags_out (optional) receives the raw flag bits.
+ */
+int32_t fedavg_check(fedavg_ctx* ctx, void* stream, uint32_t* flags_out);
+
+/*
+ * Diagnostic (error path only): for each client of the table, does any of its tensors hold
+ * NaN? out_bad[num_clients] receives 0/1. Synchronous.
+ */
+int32_t fedavg_find_nan_clients(fedavg_ctx* ctx, const void* const* client_ptrs,
+                                int32_t in_dtype, int32_t num_clients, int32_t* out_bad,
+                                void* stream);
+
+/* Kernel timing for bench.py: when enabled, every main-kernel launch is bracketed by a pair
+ * of HIP events recorded on the launch stream. fedavg_prof_collect synchronises those
+ * events, returns the summed kernel milliseconds and the launch count, and clears them. */
+int32_t fedavg_prof_enable(fedavg_ctx* ctx, int32_t enable);
+int32_t fedavg_prof_collect(fedavg_ctx* ctx, double* total_ms, int32_t* launches);
+
+/* HBM ceiling probes (bench.py's measured copy / read roofline): mode 0 = 16-B copy of
+ * `bytes` from src to dst, mode 1 = 16-B read-only stream of src (dst: >= 8 KiB scratch). */
+int32_t fedavg_bw_probe(const void* src, int64_t bytes, void* dst, int32_t mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAVG_HIP_H */

@@ -1,0 +1,85 @@
+"""Readers for the golden fixtures generated from the reference (tests/golden/gen_golden.py)."""
+
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Any
+
+import numpy as np
+import torch
+
+GOLDEN_DIR = Path(__file__).resolve().parent / "golden"
+
+
+@dataclass
+class Arrival:
+    worker_id: int
+    weight: Any
+    other_data: dict
+    arrays: dict[str, np.ndarray] | None  # raw (bf16 as uint16 bits)
+
+
+@dataclass
+class GoldenCase:
+    name: str
+    dtype: str
+    names: list[str]
+    shapes: list[tuple[int, ...]]
+    accumulate: bool
+    aggregate_loss: bool
+    per_tensor_weight: dict | None
+    arrivals: list[Arrival]
+    error: str | None
+    expected: dict[str, np.ndarray] | None
+    meta: dict
+
+    def torch_params(self, arrival: Arrival, device: torch.device | str = "cpu") -> dict[str, torch.Tensor]:
+        assert arrival.arrays is not None
+        out = {}
+        for k, a in arrival.arrays.items():
+            if self.dtype == "bfloat16":
+                t = torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
+            else:
+                t = torch.from_numpy(a.copy())
+            out[k] = t.to(device)
+        return out
+
+
+def load_golden() -> dict[str, GoldenCase]:
+    manifest = json.loads((GOLDEN_DIR / "manifest.json").read_text())
+    data = np.load(GOLDEN_DIR / "fedavg_golden.npz", allow_pickle=False)
+    cases = {}
+    for c in manifest["cases"]:
+        name = c["name"]
+        arrivals = []
+        for j, a in enumerate(c["arrivals"]):
+            arrays = None
+            if a["keys"] is not None:
+                arrays = {k: data[f"{name}/in/{j}/{k}"] for k in a["keys"]}
+            arrivals.append(Arrival(a["worker_id"], a["weight"], dict(a["other_data"]), arrays))
+        expected = None
+        if c["error"] is None:
+            expected = {k: data[f"{name}/out/{k}"] for k in c["out_keys"]}
+        cases[name] = GoldenCase(
+            name=name,
+            dtype=c["dtype"],
+            names=c["names"],
+            shapes=[tuple(s) for s in c["shapes"]],
+            accumulate=c["accumulate"],
+            aggregate_loss=c["aggregate_loss"],
+            per_tensor_weight=c["per_tensor_weight"],
+            arrivals=arrivals,
+            error=c["error"],
+            expected=expected,
+            meta=c,
+        )
+    return cases
+
+
+def bits_equal(a: np.ndarray, b: np.ndarray) -> bool:
+    """Bit-for-bit equality of float64 arrays (distinguishes -0.0 / +0.0, NaN payloads)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64))

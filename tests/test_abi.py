@@ -1,0 +1,41 @@
+"""The C ABI surface: header <-> binding <-> exported symbols (CPU only, no compute calls)."""
+
+import re
+import subprocess
+from pathlib import Path
+
+from distributed_learning_simulation_lib_amd import _native
+from distributed_learning_simulation_lib_amd.build import LIB_PATH, build
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "fedavg_hip.h"
+
+
+def header_functions() -> set[str]:
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"\b(fedavg_[a-z0-9_]+)\s*\(", text))
+
+
+def test_binding_covers_header_exactly():
+    assert header_functions() == set(_native.SIGNATURES)
+
+
+def test_library_builds_loads_and_exports_every_symbol():
+    build()  # no-op when up to date; hipcc cross-compiles gfx950 without a GPU
+    assert LIB_PATH.exists()
+    lib = _native.load()
+    assert lib.fedavg_abi_version() == _native.ABI_VERSION
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(LIB_PATH)], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (fedavg_[a-z0-9_]+)\b", nm.stdout))
+    assert header_functions() <= exported
+
+
+def test_gfx950_code_object_present():
+    # the offload bundle embedded in .hip_fatbin names its target
+    assert b"amdgcn-amd-amdhsa--gfx950" in LIB_PATH.read_bytes()
+
+
+def test_null_context_is_rejected_without_a_gpu():
+    lib = _native.load()
+    assert lib.fedavg_reset(None, None) == _native.ERR_INVALID
+    assert "null context" in _native.last_error()

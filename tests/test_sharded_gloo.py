@@ -1,0 +1,151 @@
+"""Multi-rank FedAvg (clients sharded over ranks + chunked reduce) on CPU with gloo.
+
+Covers ``sharded.sharded_reduce`` — chunking, the reduce of fp64 partials to the root, the
+weight totals and the per-chunk finalize — with world_size 2 and 3 on the CPU. The per-rank
+compute is a plain torch stand-in for the HIP reducer (same tile geometry as the native
+library: 2048-element tiles that never cross a tensor, 16-byte aligned accumulator
+segments); the GPU parity tests cover the HIP reducer itself.
+"""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_learning_simulation_lib_amd.fedavg import ModelLayout
+from distributed_learning_simulation_lib_amd.sharded import chunk_bounds, sharded_reduce
+from oracle.fedavg_oracle import fedavg_flat
+
+TILE = 2048
+
+
+class TorchCPUReducer:
+    def __init__(self, layout: ModelLayout, clients, weights, outs):
+        self.layout = layout
+        self.clients = clients  # list of list[tensor] (per segment)
+        self.weights = weights  # list of list[float]
+        self.outs = outs
+        offs, total = layout.padded_offsets(8)
+        self.acc_off = offs
+        self.accumulator = torch.zeros(total, dtype=torch.float64)
+        self.tiles = [(s, st, min(TILE, n - st)) for s, n in enumerate(layout.numels) for st in range(0, n, TILE)]
+        self.totals = None
+
+    @property
+    def num_tiles(self):
+        return len(self.tiles)
+
+    def tile_range(self, tb, te):
+        s0, st0, _ = self.tiles[tb]
+        s1, st1, c1 = self.tiles[te - 1]
+        end = self.acc_off[s1] + st1 + c1
+        if st1 + c1 == self.layout.numels[s1]:
+            end = self.acc_off[s1 + 1] if s1 + 1 < self.layout.num_segments else self.accumulator.numel()
+        return self.acc_off[s0] + st0, end
+
+    def partial(self, tb, te):
+        for s, st, c in self.tiles[tb:te]:
+            dst = self.accumulator[self.acc_off[s] + st : self.acc_off[s] + st + c]
+            dst.zero_()
+            for row, w in zip(self.clients, self.weights):
+                dst += row[s][st : st + c].double() * w[s]
+
+    def set_accumulated(self, totals):
+        self.totals = list(totals)
+
+    def finalize_range(self, tb, te):
+        for s, st, c in self.tiles[tb:te]:
+            src = self.accumulator[self.acc_off[s] + st : self.acc_off[s] + st + c]
+            self.outs[s][st : st + c] = src / self.totals[s]
+
+    def fused(self):
+        self.partial(0, self.num_tiles)
+        self.set_accumulated([sum(w[s] for w in self.weights) for s in range(self.layout.num_segments)])
+        self.finalize_range(0, self.num_tiles)
+
+
+LAYOUT = ModelLayout(names=("a", "b", "c", "d"), shapes=((5000,), (3, 7), (4096,), (2049,)))
+
+
+def make_all_clients(n):
+    g = torch.Generator().manual_seed(5)
+    clients = [[torch.randn(m, generator=g) for m in LAYOUT.numels] for _ in range(n)]
+    rng = np.random.default_rng(6)
+    weights = [[float(rng.integers(100, 5000))] * LAYOUT.num_segments for _ in range(n)]
+    return clients, weights
+
+
+def _worker(rank, world, port, n_clients, chunks, pass_totals, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        clients, weights = make_all_clients(n_clients)
+        mine = [i for i in range(n_clients) if i % world == rank]
+        outs = [torch.empty(m, dtype=torch.float64) for m in LAYOUT.numels] if rank == 0 else None
+        red = TorchCPUReducer(LAYOUT, [clients[i] for i in mine], [weights[i] for i in mine], outs)
+        local = [sum(weights[i][s] for i in mine) for s in range(LAYOUT.num_segments)]
+        glob = [sum(w[s] for w in weights) for s in range(LAYOUT.num_segments)] if pass_totals else None
+        totals = sharded_reduce(red, local, chunks=chunks, global_total_weights=glob)
+        if rank == 0:
+            q.put(("ok", [o.numpy() for o in outs], totals))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put(("err", repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,chunks,pass_totals", [(2, 4, True), (2, 1, False), (3, 3, False)])
+def test_sharded_reduce_gloo(world, chunks, pass_totals):
+    n_clients = 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_clients, chunks, pass_totals, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    status, outs, totals = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert status == "ok", outs
+    clients, weights = make_all_clients(n_clients)
+    for s in range(LAYOUT.num_segments):
+        want = fedavg_flat([c[s].numpy() for c in clients], [w[s] for w in weights])
+        mag = sum(np.abs(c[s].numpy().astype(np.float64)) * w[s] for c, w in zip(clients, weights)) / totals[s]
+        assert np.all(np.abs(outs[s] - want) <= 1e-12 * mag)
+        assert np.array_equal(outs[s].astype(np.float32), want.astype(np.float32)) or np.all(
+            np.abs(outs[s].astype(np.float32) - want.astype(np.float32)) <= np.spacing(np.abs(want.astype(np.float32)))
+        )
+
+
+def test_single_rank_uses_the_fused_path():
+    clients, weights = make_all_clients(3)
+    outs = [torch.empty(m, dtype=torch.float64) for m in LAYOUT.numels]
+    red = TorchCPUReducer(LAYOUT, clients, weights, outs)
+    totals = sharded_reduce(red, [sum(w[s] for w in weights) for s in range(4)])
+    assert len(totals) == 4
+    for s in range(4):
+        want = fedavg_flat([c[s].numpy() for c in clients], [w[s] for w in weights])
+        np.testing.assert_allclose(outs[s].numpy(), want, rtol=1e-14)
+
+
+def test_chunk_bounds_partition_tiles():
+    for n in (1, 2, 7, 100, 5709):
+        for c in (1, 2, 3, 4, 8, 1000):
+            b = chunk_bounds(n, c)
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+            assert all(x[1] > x[0] for x in b)

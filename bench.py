@@ -42,6 +42,7 @@ from distributed_learning_simulation_lib_amd.fedavg import (  # noqa: E402
     ClientTable,
     FedAvgContext,
     ModelLayout,
+    OutputTable,
     bw_probe,
 )
 from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, sharded_reduce  # noqa: E402
@@ -134,7 +135,7 @@ def cpu_baseline(layout: ModelLayout, budget_s: float = 12.0, sample_clients: in
     nbytes = (sample_clients + 1) * layout.total_numel * 4
     times = []
     t_start = time.perf_counter()
-    while time.perf_counter() - t_start < budget_s and len(times) < 50:
+    while time.perf_counter() - t_start < budget_s and len(times) < 1000:
         algo = RefOpsFedAvg()
         t0 = time.perf_counter()
         for c, w in zip(clients, weights):
@@ -198,7 +199,7 @@ def main() -> int:
     if rank == 0:
         offs, padded = layout.padded_offsets(torch.empty((), dtype=out_dtype).element_size())
         out_flat = torch.empty(padded, dtype=out_dtype, device=device)
-        outs = [out_flat[o : o + m] for o, m in zip(offs, layout.numels)]
+        outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
     reducer = HipLocalReducer(ctx, table, in_dtype, outs, out_dtype)
     local_totals = [float(sum(my_weights))] * layout.num_segments
     global_totals = [float(sum(weights_all))] * layout.num_segments

@@ -43,6 +43,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_segment_offset": (c_int64, [c_void_p, c_int32]),
     "fedavg_accumulator": (c_void_p, [c_void_p]),
     "fedavg_set_split_policy": (c_int32, [c_void_p, c_int32]),
+    "fedavg_set_fused_fold": (c_int32, [c_void_p, c_int32]),
     "fedavg_reset": (c_int32, [c_void_p, c_void_p]),
     "fedavg_total_weights": (c_int32, [c_void_p, _PD]),
     "fedavg_accumulate": (c_int32, [c_void_p, _PP, c_int32, _PD, c_int32, c_void_p]),

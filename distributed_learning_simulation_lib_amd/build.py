@@ -48,20 +48,26 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > mtime for p in SOURCES + HEADERS + [Path(__file__)])
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile the HIP library for gfx950. Returns the path of the shared object."""
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines: dict[str, int] | None = None,
+          out: Path | None = None) -> Path:
+    """Compile the HIP library for gfx950. Returns the path of the shared object.
+
+    ``defines``/``out`` build a tuning variant (e.g. ``{"FEDAVG_NT": 1}``) to another path.
+    """
+    target = out or LIB_PATH
+    if out is None and not defines and not force and not needs_build():
         return LIB_PATH
-    LIB_DIR.mkdir(parents=True, exist_ok=True)
-    tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [hipcc(), *HIPCC_FLAGS, f"-I{REPO_DIR / 'include'}", *map(str, SOURCES), "-o", str(tmp)]
+    target.parent.mkdir(parents=True, exist_ok=True)
+    tmp = target.with_suffix(".so.tmp")
+    dflags = [f"-D{k}={v}" for k, v in (defines or {}).items()]
+    cmd = [hipcc(), *HIPCC_FLAGS, *dflags, f"-I{REPO_DIR / 'include'}", *map(str, SOURCES), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd))
     proc = subprocess.run(cmd, capture_output=True, text=True)
     if proc.returncode != 0:
         raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

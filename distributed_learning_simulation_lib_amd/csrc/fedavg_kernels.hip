@@ -30,6 +30,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/fedavg_hip.h"
@@ -57,9 +58,39 @@ int32_t fail(int32_t code, const std::string& msg) {
 // ---------------------------------------------------------------------------------------
 // device-side descriptors
 // ---------------------------------------------------------------------------------------
-constexpr int kThreads = 256;     // 4 waves of 64
-constexpr int kAE = 8;            // elements owned by one lane (fp64 accumulators per lane)
-constexpr int kTile1 = kThreads * kAE;        // 2048 elements, SPLIT = 1
+#ifndef FEDAVG_THREADS1
+#define FEDAVG_THREADS1 256
+#endif
+constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
+constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
+// Tuning knobs (compile-time; the shipped values were picked on MI355X by
+// scripts/tune_kernel.py, see DESIGN.md "Kernel tuning"):
+//   FEDAVG_AE        elements owned by one lane (= fp64 accumulators per lane)
+//   FEDAVG_CU_BYTES  bytes of client loads in flight per lane per group
+//   FEDAVG_NT        1 = non-temporal (streaming) client loads
+//   FEDAVG_LOAD_FENCE 1 = sched_barrier between a group's loads and its folds
+//   FEDAVG_NT_STORE  1 = non-temporal result / accumulator stores
+// Measured on MI355X (64 x ResNet-18 fp32 -> fp32, interleaved A/B in one process):
+// nt loads ~+1-2 %, nt stores +5-9 % (a read stream with interleaved writes loses HBM
+// efficiency; nt stores cut that), AE 16 / CU 512 B +-1 %, load fence / 128-512-thread
+// groups / fused fold within noise. Shipped: AE 8, CU 256 B, nt loads and stores.
+#ifndef FEDAVG_AE
+#define FEDAVG_AE 8
+#endif
+#ifndef FEDAVG_CU_BYTES
+#define FEDAVG_CU_BYTES 256
+#endif
+#ifndef FEDAVG_NT
+#define FEDAVG_NT 1
+#endif
+#ifndef FEDAVG_LOAD_FENCE
+#define FEDAVG_LOAD_FENCE 0
+#endif
+#ifndef FEDAVG_NT_STORE
+#define FEDAVG_NT_STORE 1
+#endif
+constexpr int kAE = FEDAVG_AE;    // elements owned by one lane (fp64 accumulators per lane)
+constexpr int kTile1 = kThreads1 * kAE;       // 2048 elements, SPLIT = 1
 constexpr int kTile4 = (kThreads / 4) * kAE;  // 512 elements,  SPLIT = 4
 
 struct TileDesc {
@@ -248,7 +279,13 @@ struct LaneLoader {
   __device__ __forceinline__ static void load_raw(gptr<const T> base, int li, V (&buf)[VPL]) {
     const gptr<const V> vb = (gptr<const V>)base;
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) buf[v] = vb[v * LANES + li];
+    for (int v = 0; v < VPL; ++v) {
+#if FEDAVG_NT
+      buf[v] = __builtin_nontemporal_load(vb + v * LANES + li);
+#else
+      buf[v] = vb[v * LANES + li];
+#endif
+    }
   }
 
   // bounds-checked loads straight to doubles (segment tails, unaligned buffers)
@@ -269,15 +306,47 @@ struct LaneLoader {
 };
 
 // One tile of the weighted reduce. See the file header for the algorithm.
-template <typename T, int OUT, int SPLIT, bool VEC, bool FULL>
+// NaN flags live in host-coherent pinned memory, one word per condition (0: accumulator NaN,
+// 1: result NaN). A wave that sees a NaN stores 1 with system scope — no atomics, every
+// writer writes the same value — and the host reads the words after the stream drains.
+__device__ __forceinline__ void raise_flag(uint32_t* flag, int word) {
+  __hip_atomic_store(flag + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Vector store of a result/accumulator slice (non-temporal when FEDAVG_NT_STORE).
+template <typename V>
+__device__ __forceinline__ void store_out(gptr<V> p, V v) {
+#if FEDAVG_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// One fp64 fold step. The reference rounds the product and the sum separately
+// (`tmp = x.to(f64) * w; acc += tmp`). When the host has proven every product of the call
+// exact in fp64 (FMA = true: the weight's significand fits beside the input's, e.g. integer
+// dataset sizes and fp32 inputs), round(acc + x*w) == fma(x, w, acc) and one instruction does
+// it; otherwise the two roundings are kept.
+template <bool FMA>
+__device__ __forceinline__ double fold(double acc, double x, double w) {
+  if constexpr (FMA) {
+    return __builtin_fma(x, w, acc);
+  } else {
+    const double p = x * w;
+    return acc + p;
+  }
+}
+
+template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, bool FMA>
 __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
-  constexpr int LANES = kThreads / SPLIT;  // lanes sharing one client stream
+  constexpr int LANES = (SPLIT == 1) ? kThreads1 : kThreads / SPLIT;  // lanes sharing one client stream
   using LL = LaneLoader<T, LANES, FULL && VEC, VEC>;
   using V = typename LL::V;
   constexpr int N = LL::N;
   constexpr int VPL = LL::VPL;
   // clients in flight per lane: 256 B of loads per lane per group
-  constexpr int CU_LOADS = (256 / (VPL * 16)) < 2 ? 2 : (256 / (VPL * 16));
+  constexpr int CU_LOADS = (FEDAVG_CU_BYTES / (VPL * 16)) < 2 ? 2 : (FEDAVG_CU_BYTES / (VPL * 16));
   constexpr bool FAST = FULL && VEC;
 
   const int seg = td.seg;
@@ -300,7 +369,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     return to_global<T>(reinterpret_cast<const void*>(cp[k] + elem_off));
   };
 
-  double acc[kAE];
+  double acc[kAE] = {};
   bool have = false;  // wave-uniform
   if (SPLIT == 1 || wave == 0) {
     if (a.zero_init) {
@@ -328,34 +397,26 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     }
   }
 
-  int k = kb;
-  if (!have && k < ke) {
-    // first contribution is an assignment (fed_avg_algorithm.py:55-56), not 0 + tmp
-    const double wk = wp[k];
-    double x[kAE];
-    if constexpr (FAST) {
-      V buf[VPL];
-      LL::load_raw(client(k), li, buf);
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) expand<T>(buf[v], x + v * N);
-    } else {
-      LL::load_checked(client(k), li, count, x);
-    }
-#pragma unroll
-    for (int i = 0; i < kAE; ++i) acc[i] = x[i] * wk;
-    have = true;
-    ++k;
-  }
+  // Fold this wave's clients [kb, ke) in order, in groups of CU_LOADS clients: all loads of
+  // a group are issued before any is consumed. Group variants are compile-time: FIRST (the
+  // group's first client is an assignment, fed_avg_algorithm.py:55-56) and TAIL (a short last
+  // group: missing slots re-load the group's last client — L2 hits — and are masked out of
+  // the fold by selects, never by branches, so the compiler keeps every load in flight).
   if constexpr (FAST) {
-    // main loop: CU_LOADS clients' loads in flight, then fold them in client order
-    for (; k + CU_LOADS <= ke; k += CU_LOADS) {
+    auto group = [&](auto first_tag, auto tail_tag, int k, int n) {
+      constexpr bool FIRST = decltype(first_tag)::value;
+      constexpr bool TAIL = decltype(tail_tag)::value;
       V buf[CU_LOADS][VPL];
       double wk[CU_LOADS];
 #pragma unroll
       for (int c = 0; c < CU_LOADS; ++c) {
-        wk[c] = wp[k + c];
-        LL::load_raw(client(k + c), li, buf[c]);
+        const int kc = TAIL ? k + min(c, n - 1) : k + c;
+        wk[c] = wp[kc];
+        LL::load_raw(client(kc), li, buf[c]);
       }
+#if FEDAVG_LOAD_FENCE
+      __builtin_amdgcn_sched_barrier(0);  // every load of the group issues before any fold
+#endif
 #pragma unroll
       for (int c = 0; c < CU_LOADS; ++c) {
 #pragma unroll
@@ -364,39 +425,43 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
           expand<T>(buf[c][v], x);
 #pragma unroll
           for (int j = 0; j < N; ++j) {
-            const double prod = x[j] * wk[c];
-            acc[v * N + j] = acc[v * N + j] + prod;
+            double& r = acc[v * N + j];
+            const double nv = (FIRST && c == 0) ? x[j] * wk[c] : fold<FMA>(r, x[j], wk[c]);
+            if constexpr (TAIL) {
+              r = (c < n) ? nv : r;
+            } else {
+              r = nv;
+            }
           }
         }
       }
-    }
-    for (; k < ke; ++k) {
-      const double wk = wp[k];
-      V buf[VPL];
-      LL::load_raw(client(k), li, buf);
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        double x[N];
-        expand<T>(buf[v], x);
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          const double prod = x[j] * wk;
-          acc[v * N + j] = acc[v * N + j] + prod;
-        }
+    };
+    using T1 = std::true_type;
+    using F0 = std::false_type;
+    int k = kb;
+    if (!have && k < ke) {
+      if (ke - k >= CU_LOADS) {
+        group(T1{}, F0{}, k, CU_LOADS);
+        k += CU_LOADS;
+      } else {
+        group(T1{}, T1{}, k, ke - k);
+        k = ke;
       }
     }
+    for (; k + CU_LOADS <= ke; k += CU_LOADS) group(F0{}, F0{}, k, CU_LOADS);
+    if (k < ke) group(F0{}, T1{}, k, ke - k);
   } else {
-    for (; k < ke; ++k) {
+    bool first = !have;
+    for (int k = kb; k < ke; ++k) {
       const double wk = wp[k];
       double x[kAE];
       LL::load_checked(client(k), li, count, x);
 #pragma unroll
-      for (int i = 0; i < kAE; ++i) {
-        const double prod = x[i] * wk;
-        acc[i] = acc[i] + prod;
-      }
+      for (int i = 0; i < kAE; ++i) acc[i] = first ? x[i] * wk : fold<FMA>(acc[i], x[i], wk);
+      first = false;
     }
   }
+  have = have || (ke > kb);
 
   if constexpr (SPLIT > 1) {
     // stage wave partials in LDS; wave 0 folds them in wave order
@@ -446,14 +511,14 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
       for (int j = 0; j < N; j += 2) {
         if (FULL || e + j + 2 <= count) {
-          *(gptr<f64x2>)(ap + e + j) = f64x2{acc[v * N + j], acc[v * N + j + 1]};
+          store_out((gptr<f64x2>)(ap + e + j), f64x2{acc[v * N + j], acc[v * N + j + 1]});
         } else {
           if (e + j < count) ap[e + j] = acc[v * N + j];
           if (e + j + 1 < count) ap[e + j + 1] = acc[v * N + j + 1];
         }
       }
     }
-    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) atomicOr(a.flag, FEDAVG_FLAG_ACC_NAN);
+    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) raise_flag(a.flag, 0);
   } else {
     // fused divide (_apply_total_weight, :71-74) + NaN check of the result (:97)
     const double W = to_const<double>(a.tab.wtot)[seg];
@@ -480,9 +545,9 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
           for (int j = 0; j < N; j += 4) {
             if (VEC && (FULL || e + j + 4 <= count)) {
-              *(gptr<f32x4>)(op + e + j) =
+              store_out((gptr<f32x4>)(op + e + j),
                   f32x4{static_cast<float>(res[v * N + j]), static_cast<float>(res[v * N + j + 1]),
-                        static_cast<float>(res[v * N + j + 2]), static_cast<float>(res[v * N + j + 3])};
+                        static_cast<float>(res[v * N + j + 2]), static_cast<float>(res[v * N + j + 3])});
             } else {
 #pragma unroll
               for (int q = 0; q < 4; ++q)
@@ -491,8 +556,8 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
           }
         } else {
           if (VEC && (FULL || e + 2 <= count)) {
-            *(gptr<f32x2>)(op + e) =
-                f32x2{static_cast<float>(res[v * N]), static_cast<float>(res[v * N + 1])};
+            store_out((gptr<f32x2>)(op + e),
+                      f32x2{static_cast<float>(res[v * N]), static_cast<float>(res[v * N + 1])});
           } else {
             if (e < count) op[e] = static_cast<float>(res[v * N]);
             if (e + 1 < count) op[e + 1] = static_cast<float>(res[v * N + 1]);
@@ -507,7 +572,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
         for (int j = 0; j < N; j += 2) {
           if (VEC && (FULL || e + j + 2 <= count)) {
-            *(gptr<f64x2>)(op + e + j) = f64x2{res[v * N + j], res[v * N + j + 1]};
+            store_out((gptr<f64x2>)(op + e + j), f64x2{res[v * N + j], res[v * N + j + 1]});
           } else {
             if (e + j < count) op[e + j] = res[v * N + j];
             if (e + j + 1 < count) op[e + j + 1] = res[v * N + j + 1];
@@ -518,20 +583,21 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     const uint64_t ba = __ballot(bad_acc);
     const uint64_t br = __ballot(bad_res);
     if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
-      atomicOr(a.flag, (ba ? FEDAVG_FLAG_ACC_NAN : 0u) | (br ? FEDAVG_FLAG_RESULT_NAN : 0u));
+      if (ba) raise_flag(a.flag, 0);
+      if (br) raise_flag(a.flag, 1);
     }
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC>
-__global__ __launch_bounds__(kThreads) void fedavg_tile_kernel(KArgs a) {
+template <typename T, int OUT, int SPLIT, bool VEC, bool FMA>
+__global__ __launch_bounds__((SPLIT == 1) ? kThreads1 : kThreads) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
   const TileDesc td = load_tile(a.tiles, a.tile_begin + blockIdx.x);
-  constexpr int TILE = kThreads / SPLIT * kAE;
+  constexpr int TILE = ((SPLIT == 1) ? kThreads1 : kThreads / SPLIT) * kAE;
   if (td.count == TILE) {
-    tile_body<T, OUT, SPLIT, VEC, true>(a, td, lds);
+    tile_body<T, OUT, SPLIT, VEC, true, FMA>(a, td, lds);
   } else {
-    tile_body<T, OUT, SPLIT, VEC, false>(a, td, lds);
+    tile_body<T, OUT, SPLIT, VEC, false, FMA>(a, td, lds);
   }
 }
 
@@ -553,30 +619,43 @@ __global__ __launch_bounds__(kThreads) void nan_scan_kernel(const TileDesc* tile
   if (__ballot(b) != 0ull && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned*>(bad + k), 1u);
 }
 
-// Bandwidth probes (the measured HBM ceiling next to the roofline): mode 0 = float4 copy,
-// mode 1 = float4 read-only stream (xor-folded into one word per workgroup).
-__global__ __launch_bounds__(kThreads) void bw_copy_kernel(const float4* __restrict__ src,
-                                                          float4* __restrict__ dst, int64_t n) {
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
-    dst[i] = src[i];
+// Bandwidth probes (the measured HBM ceiling next to the roofline, and the known byte counts
+// that calibrate FETCH_SIZE / WRITE_SIZE for the main kernel's access pattern): mode 0 =
+// 16-B/lane copy, mode 1 = 16-B/lane read-only stream; both non-temporal like the main kernel,
+// 8 loads in flight per lane.
+__global__ __launch_bounds__(kThreads) void bw_copy_kernel(const f32x4* __restrict__ src,
+                                                          f32x4* __restrict__ dst, int64_t n) {
+  constexpr int G = 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads * G;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * kThreads * G; base < n; base += stride) {
+    f32x4 v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + g * kThreads + threadIdx.x;
+      if (i < n) v[g] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + g * kThreads + threadIdx.x;
+      if (i < n) __builtin_nontemporal_store(v[g], dst + i);
+    }
   }
 }
-__global__ __launch_bounds__(kThreads) void bw_read_kernel(const float4* __restrict__ src,
+__global__ __launch_bounds__(kThreads) void bw_read_kernel(const f32x4* __restrict__ src,
                                                           uint32_t* __restrict__ dst, int64_t n) {
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  constexpr int G = 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads * G;
   uint32_t x = 0;
-  int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    x ^= __float_as_uint(a.x) ^ __float_as_uint(a.y) ^ __float_as_uint(a.z) ^ __float_as_uint(a.w);
-    x ^= __float_as_uint(b.x) ^ __float_as_uint(b.y) ^ __float_as_uint(b.z) ^ __float_as_uint(b.w);
-    x ^= __float_as_uint(c.x) ^ __float_as_uint(c.y) ^ __float_as_uint(c.z) ^ __float_as_uint(c.w);
-    x ^= __float_as_uint(d.x) ^ __float_as_uint(d.y) ^ __float_as_uint(d.z) ^ __float_as_uint(d.w);
-  }
-  for (; i < n; i += stride) {
-    const float4 a = src[i];
-    x ^= __float_as_uint(a.x) ^ __float_as_uint(a.y) ^ __float_as_uint(a.z) ^ __float_as_uint(a.w);
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * kThreads * G; base < n; base += stride) {
+    f32x4 v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + g * kThreads + threadIdx.x;
+      v[g] = (i < n) ? __builtin_nontemporal_load(src + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      x ^= __float_as_uint(v[g].x) ^ __float_as_uint(v[g].y) ^ __float_as_uint(v[g].z) ^ __float_as_uint(v[g].w);
   }
   if (x == 0x9e3779b9u) dst[blockIdx.x] = x;  // practically never taken; keeps loads live
 }
@@ -600,8 +679,8 @@ struct fedavg_ctx {
   TileDesc* d_tiles1 = nullptr;
   TileDesc* d_tiles4 = nullptr;
   SegDesc* d_segs = nullptr;
-  uint32_t* d_flag = nullptr;
-  uint32_t* h_flag = nullptr;  // pinned
+  uint32_t* h_flag = nullptr;  // host-coherent pinned NaN words (kernels store into them)
+  uint32_t* d_flag = nullptr;  // device alias of h_flag
 
   // accumulated state (host mirror)
   std::vector<double> wsum;     // per-segment total weight (fed_avg_algorithm.py:59-62)
@@ -617,8 +696,12 @@ struct fedavg_ctx {
     bool used = false;
   } slots[kSlots];
   int next_slot = 0;
+  int last_slot = -1;             // slot holding last_blob on the device
+  std::vector<char> last_blob;    // host image of the last uploaded table blob
+  std::vector<char> scratch;
 
   int split_policy = 1;  // 1 exact client order (default), 0 auto, 2 always split
+  bool allow_fma = true;  // fused fold when every product is provably exact
   // profiling
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -668,9 +751,41 @@ struct Staged {
   CallTables tab;
   int32_t Kmax = 0;
   int32_t stride = 1;    // row stride of the [T][K] tables
-  bool aligned = true;   // every client/out pointer is 16-byte aligned
+  bool aligned = true;
+  int32_t max_weight_bits = 0;  // largest significand (bits) among the call's weights
+  bool weights_tame = true;     // every weight finite, zero or within [2^-800, 2^800]   // every client/out pointer is 16-byte aligned
   std::vector<int32_t> kseg;
 };
+
+// Significand width of a weight (bits between its leading and trailing one).
+void note_weight(Staged& st, double w) {
+  if (w == 0.0) return;
+  if (!std::isfinite(w)) {
+    st.weights_tame = false;
+    return;
+  }
+  int e = 0;
+  const double m = std::frexp(std::fabs(w), &e);  // m in [0.5, 1)
+  if (e < -800 || e > 800) st.weights_tame = false;
+  uint64_t bits = static_cast<uint64_t>(std::ldexp(m, 53));  // exact: 53-bit integer
+  const int q = 53 - __builtin_ctzll(bits);
+  st.max_weight_bits = std::max(st.max_weight_bits, q);
+}
+
+int32_t significand_bits(int32_t dt) {
+  switch (dt) {
+    case FEDAVG_F32: return 24;
+    case FEDAVG_F16: return 11;
+    case FEDAVG_BF16: return 8;
+    default: return 53;
+  }
+}
+
+// Every product x * w of the call is exact in fp64 (input significand + weight significand
+// <= 53 bits, no over/underflow), so fma(x, w, acc) rounds exactly like acc + round(x * w).
+bool fma_exact_call(const Staged& st, int32_t in_dtype) {
+  return st.weights_tame && significand_bits(in_dtype) + st.max_weight_bits <= 53;
+}
 
 // Build segment-major compacted tables in a pinned slot and enqueue their H2D copy.
 int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptrs,
@@ -686,22 +801,12 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
   const size_t off_wtot = align_up(off_outs + sizeof(void*) * T, 16);
   const size_t bytes = align_up(off_wtot + sizeof(double) * T, 256);
 
-  fedavg_ctx::Slot& sl = c->slots[c->next_slot];
-  c->next_slot = (c->next_slot + 1) % fedavg_ctx::kSlots;
-  if (sl.used) FEDAVG_HIP_TRY(hipEventSynchronize(sl.done));  // its previous copy finished
-  if (sl.cap < bytes) {
-    if (sl.host) FEDAVG_HIP_TRY(hipHostFree(sl.host));
-    if (sl.dev) {
-      FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // a kernel may still read the old table
-      FEDAVG_HIP_TRY(hipFree(sl.dev));
-    }
-    const size_t cap = std::max<size_t>(bytes * 2, 64 * 1024);
-    FEDAVG_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sl.host), cap, hipHostMallocDefault));
-    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.dev), cap));
-    sl.cap = cap;
-    if (!sl.done) FEDAVG_HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-  }
-  char* h = sl.host;
+  // Build the blob in host scratch first: when it is byte-identical to the previous call's
+  // (same clients, weights, outputs — e.g. persistent client slots round after round), the
+  // device copy already holds it and no upload is issued.
+  std::vector<char>& blob = c->scratch;
+  blob.assign(bytes, 0);
+  char* h = blob.data();
   const void** hp = reinterpret_cast<const void**>(h + off_ptr);
   double* hw = reinterpret_cast<double*>(h + off_w);
   int32_t* hk = reinterpret_cast<int32_t*>(h + off_kseg);
@@ -720,7 +825,9 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
       if (p == nullptr) continue;
       if (reinterpret_cast<uintptr_t>(p) % 16 != 0) st.aligned = false;
       hp[static_cast<int64_t>(t) * Kr + n] = p;
-      hw[static_cast<int64_t>(t) * Kr + n] = weights[static_cast<int64_t>(k) * T + t];
+      const double wv = weights[static_cast<int64_t>(k) * T + t];
+      hw[static_cast<int64_t>(t) * Kr + n] = wv;
+      note_weight(st, wv);
       ++n;
     }
     hk[t] = n;
@@ -731,11 +838,37 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
     if (out_ptrs && reinterpret_cast<uintptr_t>(out_ptrs[t]) % 16 != 0) st.aligned = false;
     hwt[t] = wtot ? wtot[t] : 1.0;
   }
-  FEDAVG_HIP_TRY(hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, s));
-  FEDAVG_HIP_TRY(hipEventRecord(sl.done, s));
-  sl.used = true;
 
-  char* d = sl.dev;
+  char* d = nullptr;
+  if (c->last_slot >= 0 && c->last_blob.size() == bytes &&
+      std::memcmp(c->last_blob.data(), blob.data(), bytes) == 0) {
+    d = c->slots[c->last_slot].dev;  // unchanged since it was uploaded on this stream
+  } else {
+    const int slot = c->next_slot;
+    fedavg_ctx::Slot& sl = c->slots[slot];
+    c->next_slot = (c->next_slot + 1) % fedavg_ctx::kSlots;
+    if (sl.used) FEDAVG_HIP_TRY(hipEventSynchronize(sl.done));  // its previous copy finished
+    if (sl.cap < bytes) {
+      if (sl.host) FEDAVG_HIP_TRY(hipHostFree(sl.host));
+      if (sl.dev) {
+        FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // a kernel may still read the old table
+        FEDAVG_HIP_TRY(hipFree(sl.dev));
+      }
+      const size_t cap = std::max<size_t>(bytes * 2, 64 * 1024);
+      FEDAVG_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sl.host), cap, hipHostMallocDefault));
+      FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.dev), cap));
+      sl.cap = cap;
+      if (!sl.done) FEDAVG_HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    std::memcpy(sl.host, blob.data(), bytes);
+    FEDAVG_HIP_TRY(hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, s));
+    FEDAVG_HIP_TRY(hipEventRecord(sl.done, s));
+    sl.used = true;
+    c->last_blob.swap(blob);
+    c->last_slot = slot;
+    d = sl.dev;
+  }
+
   st.tab.cptrs = reinterpret_cast<const void* const*>(d + off_ptr);
   st.tab.w = reinterpret_cast<const double*>(d + off_w);
   st.tab.kseg = reinterpret_cast<const int32_t*>(d + off_kseg);
@@ -745,25 +878,29 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
   return FEDAVG_OK;
 }
 
-template <typename T, int OUT>
-hipError_t launch_typed(const KArgs& a, int split, bool vec, int nblocks, hipStream_t s) {
-  if (split == 4) {
-    if (vec) hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 4, true>), dim3(nblocks), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 4, false>), dim3(nblocks), dim3(kThreads), 0, s, a);
-  } else {
-    if (vec) hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, true>), dim3(nblocks), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, false>), dim3(nblocks), dim3(kThreads), 0, s, a);
-  }
+template <typename T, int OUT, int SPLIT, bool VEC>
+hipError_t launch_fma(const KArgs& a, bool fma, int nblocks, hipStream_t s) {
+  const int threads = (SPLIT == 1) ? kThreads1 : kThreads;
+  if (fma) hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, true>), dim3(nblocks), dim3(threads), 0, s, a);
+  else hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, false>), dim3(nblocks), dim3(threads), 0, s, a);
   return hipGetLastError();
 }
 
+template <typename T, int OUT>
+hipError_t launch_typed(const KArgs& a, int split, bool vec, bool fma, int nblocks, hipStream_t s) {
+  if (split == 4) {
+    return vec ? launch_fma<T, OUT, 4, true>(a, fma, nblocks, s) : launch_fma<T, OUT, 4, false>(a, fma, nblocks, s);
+  }
+  return vec ? launch_fma<T, OUT, 1, true>(a, fma, nblocks, s) : launch_fma<T, OUT, 1, false>(a, fma, nblocks, s);
+}
+
 template <int OUT>
-hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int nblocks, hipStream_t s) {
+hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, bool fma, int nblocks, hipStream_t s) {
   switch (in_dtype) {
-    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, nblocks, s);
-    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, nblocks, s);
-    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, nblocks, s);
-    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, nblocks, s);
+    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fma, nblocks, s);
+    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fma, nblocks, s);
+    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fma, nblocks, s);
+    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fma, nblocks, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -809,10 +946,11 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     FEDAVG_HIP_TRY(hipEventRecord(e0, s));
   }
   hipError_t err = hipSuccess;
+  const bool fma = c->allow_fma && fma_exact_call(st, in_dtype);
   switch (out_kind) {
-    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, nblocks, s); break;
-    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, nblocks, s); break;
-    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, nblocks, s); break;
+    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fma, nblocks, s); break;
+    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fma, nblocks, s); break;
+    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fma, nblocks, s); break;
     default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
   }
   if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
@@ -910,17 +1048,18 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
     return cleanup(e, "hipMalloc tiles4");
   if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_segs), sizeof(SegDesc) * segs.size())) != hipSuccess)
     return cleanup(e, "hipMalloc segs");
-  if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_flag), sizeof(uint32_t) * 4)) != hipSuccess)
-    return cleanup(e, "hipMalloc flag");
-  if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_flag), sizeof(uint32_t) * 4, hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_flag), sizeof(uint32_t) * 4,
+                         hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
     return cleanup(e, "hipHostMalloc flag");
+  if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_flag), c->h_flag, 0)) != hipSuccess)
+    return cleanup(e, "hipHostGetDevicePointer flag");
   if ((e = hipMemcpy(c->d_tiles1, c->tiles1.data(), sizeof(TileDesc) * c->tiles1.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "hipMemcpy tiles1");
   if ((e = hipMemcpy(c->d_tiles4, c->tiles4.data(), sizeof(TileDesc) * c->tiles4.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "hipMemcpy tiles4");
   if ((e = hipMemcpy(c->d_segs, segs.data(), sizeof(SegDesc) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "hipMemcpy segs");
-  if ((e = hipMemset(c->d_flag, 0, sizeof(uint32_t) * 4)) != hipSuccess) return cleanup(e, "hipMemset flag");
+  std::memset(c->h_flag, 0, sizeof(uint32_t) * 4);
   if (accumulator != nullptr) {
     c->acc = static_cast<double*>(accumulator);
     c->owns_acc = false;
@@ -952,7 +1091,6 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   if (c->d_tiles1) (void)hipFree(c->d_tiles1);
   if (c->d_tiles4) (void)hipFree(c->d_tiles4);
   if (c->d_segs) (void)hipFree(c->d_segs);
-  if (c->d_flag) (void)hipFree(c->d_flag);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->owns_acc && c->acc) (void)hipFree(c->acc);
   delete c;
@@ -972,6 +1110,12 @@ int32_t fedavg_set_split_policy(fedavg_ctx* c, int32_t policy) {
   FEDAVG_RET(check_ctx(c));
   if (policy < 0 || policy > 2) return fail(FEDAVG_ERR_INVALID, "split policy must be 0, 1 or 2");
   c->split_policy = policy;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_set_fused_fold(fedavg_ctx* c, int32_t enable) {
+  FEDAVG_RET(check_ctx(c));
+  c->allow_fma = enable != 0;
   return FEDAVG_OK;
 }
 
@@ -1152,9 +1296,9 @@ int32_t fedavg_check(fedavg_ctx* c, void* stream, uint32_t* flags_out) {
   FEDAVG_RET(check_ctx(c));
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  FEDAVG_HIP_TRY(hipMemcpyAsync(c->h_flag, c->d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   FEDAVG_HIP_TRY(hipStreamSynchronize(s));
-  const uint32_t f = c->h_flag[0];
+  const uint32_t f = (__atomic_load_n(&c->h_flag[0], __ATOMIC_ACQUIRE) ? FEDAVG_FLAG_ACC_NAN : 0u) |
+                     (__atomic_load_n(&c->h_flag[1], __ATOMIC_ACQUIRE) ? FEDAVG_FLAG_RESULT_NAN : 0u);
   if (flags_out) *flags_out = f;
   if (f & FEDAVG_FLAG_ACC_NAN) return fail(FEDAVG_ERR_NAN_ACCUM, "NaN in the accumulator");
   if (f & FEDAVG_FLAG_RESULT_NAN) return fail(FEDAVG_ERR_NAN_RESULT, "NaN in the aggregated result");
@@ -1231,10 +1375,10 @@ int32_t fedavg_bw_probe(const void* src, int64_t bytes, void* dst, int32_t mode,
   const int64_t n = bytes / 16;
   const int blocks = 256 * 8;
   if (mode == 0) {
-    hipLaunchKernelGGL(bw_copy_kernel, dim3(blocks), dim3(kThreads), 0, s, static_cast<const float4*>(src),
-                       static_cast<float4*>(dst), n);
+    hipLaunchKernelGGL(bw_copy_kernel, dim3(blocks), dim3(kThreads), 0, s, static_cast<const f32x4*>(src),
+                       static_cast<f32x4*>(dst), n);
   } else {
-    hipLaunchKernelGGL(bw_read_kernel, dim3(blocks), dim3(kThreads), 0, s, static_cast<const float4*>(src),
+    hipLaunchKernelGGL(bw_read_kernel, dim3(blocks), dim3(kThreads), 0, s, static_cast<const f32x4*>(src),
                        static_cast<uint32_t*>(dst), n);
   }
   FEDAVG_HIP_TRY(hipGetLastError());

@@ -119,6 +119,7 @@ class ClientTable:
         self._weights: list[float] = []
         self._keep: list[torch.Tensor] = []
         self.num_clients = 0
+        self._arrays: tuple[np.ndarray, np.ndarray] | None = None
 
     def add_client(self, tensors: Sequence[torch.Tensor | None], weights: Sequence[float]) -> None:
         if len(tensors) != self.num_segments or len(weights) != self.num_segments:
@@ -132,15 +133,36 @@ class ClientTable:
                 self._weights.append(float(w))
                 self._keep.append(t)
         self.num_clients += 1
+        self._arrays = None
 
     def arrays(self) -> tuple[np.ndarray, np.ndarray]:
-        ptrs = np.asarray(self._ptrs, dtype=np.uint64) if self._ptrs else np.zeros(1, np.uint64)
-        ws = np.asarray(self._weights, dtype=np.float64) if self._weights else np.zeros(1, np.float64)
-        return ptrs, ws
+        """The C-ABI arrays (built once per table and cached: a table can be reduced many times)."""
+        if self._arrays is None:
+            ptrs = np.asarray(self._ptrs, dtype=np.uint64) if self._ptrs else np.zeros(1, np.uint64)
+            ws = np.asarray(self._weights, dtype=np.float64) if self._weights else np.zeros(1, np.float64)
+            self._arrays = (ptrs, ws)
+        return self._arrays
 
     def rows(self) -> list[list[int]]:
         T = self.num_segments
         return [self._ptrs[k * T : (k + 1) * T] for k in range(self.num_clients)]
+
+
+class OutputTable:
+    """Validated per-segment output tensors of one dtype (built once, reusable across calls)."""
+
+    def __init__(self, outs: Sequence[torch.Tensor], layout: ModelLayout, device: torch.device,
+                 dtype: torch.dtype) -> None:
+        if len(outs) != layout.num_segments:
+            raise ValueError("one output tensor per segment is required")
+        for o, n in zip(outs, layout.numels):
+            if o.dtype != dtype or o.device != device or o.numel() != n or not o.is_contiguous():
+                raise ValueError("output tensors must be contiguous, on the context device, of the layout size")
+        self.tensors = list(outs)
+        self.dtype = dtype
+        self.layout = layout
+        self.device = device
+        self.c_array = (ctypes.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
 
 
 class FedAvgContext:
@@ -151,8 +173,9 @@ class FedAvgContext:
         layout: ModelLayout,
         device: torch.device | str | int | None = None,
         split_policy: int | None = None,
+        lib: ctypes.CDLL | None = None,
     ) -> None:
-        self._lib = _native.load()
+        self._lib = lib if lib is not None else _native.load()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         device = torch.device(device)
@@ -221,13 +244,12 @@ class FedAvgContext:
         _native.check(self._lib.fedavg_total_weights(self._h, out))
         return list(out)
 
-    def _out_table(self, outs: Sequence[torch.Tensor], out_dtype: torch.dtype) -> ctypes.Array:
-        if len(outs) != self.layout.num_segments:
-            raise ValueError("one output tensor per segment is required")
-        for o, n in zip(outs, self.layout.numels):
-            if o.dtype != out_dtype or o.device != self.device or o.numel() != n or not o.is_contiguous():
-                raise ValueError("output tensors must be contiguous, on the context device, of the layout size")
-        return (ctypes.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
+    def _out_table(self, outs: Sequence[torch.Tensor] | OutputTable, out_dtype: torch.dtype) -> ctypes.Array:
+        if isinstance(outs, OutputTable):
+            if outs.dtype != out_dtype or outs.layout != self.layout or outs.device != self.device:
+                raise ValueError("output table was built for another dtype, layout or device")
+            return outs.c_array
+        return OutputTable(outs, self.layout, self.device, out_dtype).c_array
 
     def _check_table(self, table: ClientTable, in_dtype: torch.dtype) -> None:
         if table.num_segments != self.layout.num_segments:
@@ -252,7 +274,7 @@ class FedAvgContext:
         self,
         table: ClientTable | None,
         in_dtype: torch.dtype,
-        outs: Sequence[torch.Tensor],
+        outs: Sequence[torch.Tensor] | OutputTable,
         out_dtype: torch.dtype,
     ) -> None:
         """Fold the last wave (optional) then out = acc / total_weight (fed_avg_algorithm.py:76-99)."""
@@ -317,6 +339,10 @@ class FedAvgContext:
         _native.check(
             self._lib.fedavg_finalize_range(self._h, ot, out_code(out_dtype), tile_begin, tile_end, self.stream)
         )
+
+    def set_fused_fold(self, enable: bool) -> None:
+        """Allow the one-instruction fold when every product is provably exact (default on)."""
+        _native.check(self._lib.fedavg_set_fused_fold(self._h, 1 if enable else 0))
 
     def reset(self) -> None:
         _native.check(self._lib.fedavg_reset(self._h, self.stream))

@@ -100,6 +100,14 @@ void* fedavg_accumulator(const fedavg_ctx* ctx);
  * The split kernel reorders the fp64 sum (four wave partials combined in LDS). */
 int32_t fedavg_set_split_policy(fedavg_ctx* ctx, int32_t policy);
 
+/* Fused fold (default on): when every product x*w of a call is exact in fp64 — the weight's
+ * significand fits next to the input's (fp32 x: weights with <= 29 significant bits, e.g.
+ * integer dataset sizes < 2^29; fp16/bf16 x: <= 42 / 45 bits) — the kernel folds with one
+ * fma(x, w, acc), which rounds exactly like the reference's acc + round(x*w). Otherwise (or
+ * when disabled) the product and the sum are rounded separately. Results are identical
+ * either way; this only trades VALU work. */
+int32_t fedavg_set_fused_fold(fedavg_ctx* ctx, int32_t enable);
+
 /* Forget accumulated state and the NaN flag (AggregationAlgorithm.clear_worker_data,
  * aggregation_algorithm.py:107-109). Asynchronous on stream. */
 int32_t fedavg_reset(fedavg_ctx* ctx, void* stream);

@@ -157,6 +157,18 @@ def cpu_baseline(layout: ModelLayout, budget_s: float = 12.0, sample_clients: in
     }
 
 
+def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -> tuple[float | None, str | None]:
+    """HBM bytes per launch of the same kernel and workload from the newest committed
+    rocprofv3 PMC summary (scripts/profile.sh -> profiles/<tag>_traffic.json), or None."""
+    if world != 1 or n_local != 64 or in_dtype != "float32" or out_dtype != "float32":
+        return None, None
+    files = sorted((REPO / "profiles").glob("r*_traffic.json"))
+    if not files:
+        return None, None
+    d = json.loads(files[-1].read_text())
+    return float(d["hbm_traffic_bytes_per_launch"]), f"profiles/{files[-1].name}"
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,6 +264,7 @@ def main() -> int:
         kernel_s = kernel_ms * 1e-3 / args.steps
     achieved = launch_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
 
+    traffic, traffic_src = committed_traffic(world, n_local, args.in_dtype, args.out_dtype)
     probe = None
     cpu = None
     if rank == 0 and not args.no_probe:
@@ -297,7 +310,8 @@ def main() -> int:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "fedavg_tile_kernel<float, OUT_F32, 1, true>" if world == 1 else "fedavg_tile_kernel<float, OUT_ACC, 1, true> (+finalize)",
             "bytes_per_launch": launch_bytes,
             "mean_launch_ms": round(per_launch_ms, 4),

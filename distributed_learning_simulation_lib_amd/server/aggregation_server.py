@@ -97,6 +97,7 @@ class AggregationServer:
         self._model_cache = ModelCache()
         self._worker_flag: set[int] = set()
         self.results: list[ParameterMessage] = []
+        self.arrivals: list[list[int]] = [[]]  # worker ids in processing order, per result
         self.round_seconds: list[float] = []
         self._round_t0: float | None = None
         algorithm.set_config(config)
@@ -136,6 +137,7 @@ class AggregationServer:
                 if old_parameter is not None:
                     data.complete(old_parameter)
         self._algorithm.process_worker_data(worker_id=worker_id, worker_data=data)
+        self.arrivals[-1].append(worker_id)
         self._worker_flag.add(worker_id)
         if len(self._worker_flag) == self.worker_number:
             result = self._aggregate_worker_data()
@@ -158,6 +160,7 @@ class AggregationServer:
                 is_initial=result.is_initial,
             )
             self.results.append(result)
+            self.arrivals.append([])
         if self._round_t0 is not None:
             self.round_seconds.append(time.perf_counter() - self._round_t0)
             self._round_t0 = None

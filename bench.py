@@ -80,6 +80,58 @@ def resnet18_layout() -> ModelLayout:
     return layout
 
 
+def vitb16_layout() -> ModelLayout:
+    """torchvision ViT-B/16 named_parameters(): 152 tensors, 86,567,656 elements (config 4)."""
+    d, f = 768, 3072
+    shapes: list[tuple[str, tuple[int, ...]]] = [
+        ("class_token", (1, 1, d)), ("conv_proj.weight", (d, 3, 16, 16)), ("conv_proj.bias", (d,)),
+        ("encoder.pos_embedding", (1, 197, d)),
+    ]
+    for i in range(12):
+        p = f"encoder.layers.encoder_layer_{i}"
+        shapes += [
+            (f"{p}.ln_1.weight", (d,)), (f"{p}.ln_1.bias", (d,)),
+            (f"{p}.self_attention.in_proj_weight", (3 * d, d)), (f"{p}.self_attention.in_proj_bias", (3 * d,)),
+            (f"{p}.self_attention.out_proj.weight", (d, d)), (f"{p}.self_attention.out_proj.bias", (d,)),
+            (f"{p}.ln_2.weight", (d,)), (f"{p}.ln_2.bias", (d,)),
+            (f"{p}.mlp.0.weight", (f, d)), (f"{p}.mlp.0.bias", (f,)),
+            (f"{p}.mlp.3.weight", (d, f)), (f"{p}.mlp.3.bias", (d,)),
+        ]
+    shapes += [("encoder.ln.weight", (d,)), ("encoder.ln.bias", (d,)),
+               ("heads.head.weight", (1000, d)), ("heads.head.bias", (1000,))]
+    layout = ModelLayout(names=tuple(n for n, _ in shapes), shapes=tuple(s for _, s in shapes))
+    assert layout.num_segments == 152 and layout.total_numel == 86_567_656, layout.total_numel
+    return layout
+
+
+def gpt2s_layout() -> ModelLayout:
+    """GPT-2 small (HF GPT2Model) named_parameters(): 148 tensors, 124,439,808 elements (config 5)."""
+    d, f = 768, 3072
+    shapes: list[tuple[str, tuple[int, ...]]] = [("wte.weight", (50257, d)), ("wpe.weight", (1024, d))]
+    for i in range(12):
+        p = f"h.{i}"
+        shapes += [
+            (f"{p}.ln_1.weight", (d,)), (f"{p}.ln_1.bias", (d,)),
+            (f"{p}.attn.c_attn.weight", (d, 3 * d)), (f"{p}.attn.c_attn.bias", (3 * d,)),
+            (f"{p}.attn.c_proj.weight", (d, d)), (f"{p}.attn.c_proj.bias", (d,)),
+            (f"{p}.ln_2.weight", (d,)), (f"{p}.ln_2.bias", (d,)),
+            (f"{p}.mlp.c_fc.weight", (d, f)), (f"{p}.mlp.c_fc.bias", (f,)),
+            (f"{p}.mlp.c_proj.weight", (f, d)), (f"{p}.mlp.c_proj.bias", (d,)),
+        ]
+    shapes += [("ln_f.weight", (d,)), ("ln_f.bias", (d,))]
+    layout = ModelLayout(names=tuple(n for n, _ in shapes), shapes=tuple(s for _, s in shapes))
+    assert layout.num_segments == 148 and layout.total_numel == 124_439_808, layout.total_numel
+    return layout
+
+
+LAYOUTS = {
+    "resnet18": resnet18_layout,
+    "vitb16": vitb16_layout,
+    "gpt2s": gpt2s_layout,
+    "flat1m": lambda: ModelLayout.flat(1_000_000),
+}
+
+
 def dataset_size_weights(n: int, seed: int = 99) -> list[int]:
     rng = np.random.default_rng(seed)
     return [int(x) for x in rng.integers(100, 5001, size=n)]
@@ -174,12 +226,16 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--layout", default="resnet18", choices=sorted(LAYOUTS))
     ap.add_argument("--clients-per-gpu", type=int, default=64)
+    ap.add_argument("--wave", type=int, default=0, help="clients per launch (streaming waves); 0 = all")
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,96 +245,109 @@ def main() -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    if world > 1 or args.force_collective:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
+    sharded = world > 1 or args.force_collective
 
     in_dtype = getattr(torch, args.in_dtype)
     out_dtype = getattr(torch, args.out_dtype)
-    layout = resnet18_layout()
+    layout = LAYOUTS[args.layout]()
     P = layout.total_numel
+    T = layout.num_segments
     n_local = args.clients_per_gpu
     n_total = n_local * world
+    wave = args.wave if 0 < args.wave < n_local else n_local
     weights_all = dataset_size_weights(n_total)
     my_weights = weights_all[rank * n_local : (rank + 1) * n_local]
 
     buckets, views = make_clients(layout, rank * n_local, n_local, device, in_dtype)
-    table = ClientTable(layout.num_segments)
-    for row, w in zip(views, my_weights):
-        table.add_client(row, [w] * layout.num_segments)
+    tables = []
+    for w0 in range(0, n_local, wave):
+        t = ClientTable(T)
+        for row, w in zip(views[w0 : w0 + wave], my_weights[w0 : w0 + wave]):
+            t.add_client(row, [w] * T)
+        tables.append(t)
     ctx = FedAvgContext(layout, device)
-    out_flat = None
     outs = None
     if rank == 0:
         offs, padded = layout.padded_offsets(torch.empty((), dtype=out_dtype).element_size())
         out_flat = torch.empty(padded, dtype=out_dtype, device=device)
         outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
-    reducer = HipLocalReducer(ctx, table, in_dtype, outs, out_dtype)
-    local_totals = [float(sum(my_weights))] * layout.num_segments
-    global_totals = [float(sum(weights_all))] * layout.num_segments
+    reducer = HipLocalReducer(ctx, tables[-1], in_dtype, outs, out_dtype, prior_waves=tables[:-1])
+    local_totals = [float(sum(my_weights))] * T
+    global_totals = [float(sum(weights_all))] * T
 
     def step() -> None:
-        sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals)
+        sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals,
+                       force_collective=args.force_collective)
         if rank == 0:
             ctx.raise_on_nan()  # the reference's assertions: the round ends on the host
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(device)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     ctx.prof_collect()  # drop warmup events
     ctx.prof_enable(True)
     torch.cuda.synchronize(device)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(device)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     ctx.prof_enable(False)
     kernel_ms, launches = ctx.prof_collect()
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    in_bytes = np.dtype(np.float32).itemsize if in_dtype == torch.float32 else torch.empty((), dtype=in_dtype).element_size()
+    in_bytes = torch.empty((), dtype=in_dtype).element_size()
     out_bytes = torch.empty((), dtype=out_dtype).element_size()
     job_bytes = n_total * P * in_bytes + P * out_bytes
     step_s = elapsed / args.steps
     value_gbps = job_bytes / step_s / 1e9
 
-    # dominant kernel: N=1 -> the fused launch (clients read + output write);
-    # N>1 -> this rank's launches per step (partial chunks + finalize on root)
-    per_launch_ms = kernel_ms / max(launches, 1)
-    if world == 1:
-        launch_bytes = n_local * P * in_bytes + P * out_bytes
-        kernel_s = per_launch_ms * 1e-3
+    # dominant kernel family, per step on this rank: the client reads + the result write
+    # (fused single launch) or + the fp64 partial/accumulator traffic (waves, shards)
+    n_waves = len(tables)
+    rank_bytes = n_local * P * in_bytes
+    if not sharded:
+        rank_bytes += P * out_bytes + (n_waves - 1) * P * 16  # fp64 accumulator round trips between waves
     else:
-        launch_bytes = n_local * P * in_bytes + P * 8  # this rank's fp64 partial write
-        kernel_s = kernel_ms * 1e-3 / args.steps
-    achieved = launch_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        rank_bytes += (n_waves - 1) * P * 16 + P * 8 + (P * (8 + out_bytes) if rank == 0 else 0)
+    kernel_step_s = kernel_ms * 1e-3 / args.steps
+    achieved = rank_bytes / kernel_step_s / 1e9 if kernel_step_s > 0 else 0.0
+    per_launch_ms = kernel_ms / max(launches, 1)
 
-    traffic, traffic_src = committed_traffic(world, n_local, args.in_dtype, args.out_dtype)
+    traffic, traffic_src = (None, None)
+    if not sharded and n_waves == 1 and args.layout == "resnet18":
+        traffic, traffic_src = committed_traffic(world, n_local, args.in_dtype, args.out_dtype)
     probe = None
     cpu = None
     if rank == 0 and not args.no_probe:
         probe = hbm_probes(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        del buckets, views, table, reducer
+        del buckets, views, tables, reducer
         torch.cuda.empty_cache()
         cpu = cpu_baseline(layout)
 
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     if rank != 0:
         return 0
+    short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    kname = {torch.float32: "float", torch.float16: "__half", torch.bfloat16: "bf16_t", torch.float64: "double"}[in_dtype]
     line = {
         "metric": METRIC,
         "value": round(value_gbps, 2),
@@ -293,16 +362,19 @@ def main() -> int:
         "dtype": "f64",
         "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
         "config": {
-            "workload": "fedavg_resnet18_fp32_64_clients_per_gpu",
+            "workload": f"fedavg_{args.layout}_{short}_{n_local}_clients_per_gpu" + (f"_waves_of_{wave}" if n_waves > 1 else ""),
             "clients_per_gpu": n_local,
             "total_clients": n_total,
+            "clients_per_launch": wave,
             "params_per_client": P,
-            "tensors_per_client": layout.num_segments,
+            "tensors_per_client": T,
             "in_dtype": args.in_dtype,
             "accumulate_dtype": "float64",
             "out_dtype": args.out_dtype,
             "parallelism": "single GPU" if world == 1 else f"clients sharded over {world} GPUs + chunked RCCL reduce to rank 0",
-            "baseline_config": "BASELINE.json configs[1]" if world == 1 else "BASELINE.json configs[2] (weak-scaled, 64 clients/GPU)",
+            "baseline_config": ("BASELINE.json configs[1]" if (world == 1 and args.layout == "resnet18" and n_local == 64)
+                                else "BASELINE.json configs[2] (weak-scaled, 64 clients/GPU)" if args.layout == "resnet18"
+                                else "see DESIGN.md"),
         },
         "roofline": {
             "bound": "hbm",
@@ -312,8 +384,10 @@ def main() -> int:
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "fedavg_tile_kernel<float, OUT_F32, 1, true>" if world == 1 else "fedavg_tile_kernel<float, OUT_ACC, 1, true> (+finalize)",
-            "bytes_per_launch": launch_bytes,
+            "kernel": (f"fedavg_tile_kernel<{kname}, OUT_F32, 1, true, fma>" if not sharded and n_waves == 1
+                       else f"fedavg_tile_kernel<{kname}, ...> x {n_waves} waves" + (" + RCCL reduce + finalize" if sharded else "")),
+            "bytes_per_step_this_rank": rank_bytes,
+            "kernel_ms_per_step": round(kernel_ms / args.steps, 4),
             "mean_launch_ms": round(per_launch_ms, 4),
             "launches": launches,
         },

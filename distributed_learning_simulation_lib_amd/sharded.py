@@ -31,7 +31,7 @@ from typing import Protocol
 import torch
 import torch.distributed as dist
 
-from .fedavg import ClientTable, FedAvgContext
+from .fedavg import ClientTable, FedAvgContext, OutputTable
 
 
 class LocalReducer(Protocol):
@@ -50,23 +50,31 @@ class LocalReducer(Protocol):
 
     def fused(self) -> None: ...
 
+    def prefold(self) -> None: ...
+
 
 class HipLocalReducer:
-    """The shard's clients, reduced by the HIP kernels of one FedAvgContext."""
+    """The shard's clients, reduced by the HIP kernels of one FedAvgContext.
+
+    ``prior_waves`` are client tables folded into the accumulator before the chunked last
+    wave (streaming waves: BASELINE config 5 folds 1024 clients in waves).
+    """
 
     def __init__(
         self,
         ctx: FedAvgContext,
         table: ClientTable | None,
         in_dtype: torch.dtype,
-        outs: Sequence[torch.Tensor] | None,
+        outs: Sequence[torch.Tensor] | OutputTable | None,
         out_dtype: torch.dtype,
+        prior_waves: Sequence[ClientTable] = (),
     ) -> None:
         self.ctx = ctx
         self.table = table
         self.in_dtype = in_dtype
         self.outs = outs
         self.out_dtype = out_dtype
+        self.prior_waves = list(prior_waves)
         self.accumulator = ctx.accumulator
 
     @property
@@ -76,8 +84,15 @@ class HipLocalReducer:
     def tile_range(self, tile_begin: int, tile_end: int) -> tuple[int, int]:
         return self.ctx.tile_range(tile_begin, tile_end)
 
+    def prefold(self) -> None:
+        """Fold the prior waves (if any) into the accumulator, in order."""
+        self.ctx.reset()
+        for t in self.prior_waves:
+            self.ctx.accumulate(t, self.in_dtype)
+
     def partial(self, tile_begin: int, tile_end: int) -> None:
-        self.ctx.partial(self.table, self.in_dtype, zero_init=True, tile_begin=tile_begin, tile_end=tile_end)
+        self.ctx.partial(self.table, self.in_dtype, zero_init=not self.prior_waves,
+                         tile_begin=tile_begin, tile_end=tile_end)
 
     def set_accumulated(self, total_weights: Sequence[float]) -> None:
         self.ctx.set_accumulated(total_weights)
@@ -87,8 +102,9 @@ class HipLocalReducer:
         self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
 
     def fused(self) -> None:
-        """Single-rank shortcut: fold + divide in one launch, no fp64 round trip."""
+        """Single-rank shortcut: fold + divide in the last wave's launch, no extra fp64 pass."""
         assert self.outs is not None
+        self.prefold()
         self.ctx.aggregate(self.table, self.in_dtype, self.outs, self.out_dtype)
 
 
@@ -105,6 +121,7 @@ def sharded_reduce(
     root: int = 0,
     group: dist.ProcessGroup | None = None,
     global_total_weights: Sequence[float] | None = None,
+    force_collective: bool = False,
 ) -> list[float]:
     """One FedAvg reduce over every rank's shard; the result lands in the root's outputs.
 
@@ -112,10 +129,11 @@ def sharded_reduce(
     caller already knows the global totals (the dispatcher that assigned clients to ranks
     knows every client's weight) it passes ``global_total_weights`` and no collective is
     spent on them; otherwise they are all-reduced first. Returns the global totals. On a
-    one-rank world the fused single-launch kernel is used (no fp64 round trip).
+    one-rank world the fused single-launch kernel is used (no fp64 round trip) unless
+    ``force_collective`` (tests / measurement of the sharded path on one GPU).
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world == 1:
+    if world == 1 and not (force_collective and dist.is_initialized()):
         reducer.fused()
         return list(local_total_weights)
     rank = dist.get_rank(group)
@@ -125,6 +143,7 @@ def sharded_reduce(
         dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
         global_total_weights = totals.tolist()
     global_totals = [float(w) for w in global_total_weights]
+    reducer.prefold()
     bounds = chunk_bounds(reducer.num_tiles, chunks)
     works = []
     for tb, te in bounds:

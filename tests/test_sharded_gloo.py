@@ -64,6 +64,9 @@ class TorchCPUReducer:
             src = self.accumulator[self.acc_off[s] + st : self.acc_off[s] + st + c]
             self.outs[s][st : st + c] = src / self.totals[s]
 
+    def prefold(self):
+        pass
+
     def fused(self):
         self.partial(0, self.num_tiles)
         self.set_accumulated([sum(w[s] for w in self.weights) for s in range(self.layout.num_segments)])

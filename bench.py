@@ -234,6 +234,7 @@ def main() -> int:
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
     args = ap.parse_args()
@@ -275,7 +276,8 @@ def main() -> int:
         offs, padded = layout.padded_offsets(torch.empty((), dtype=out_dtype).element_size())
         out_flat = torch.empty(padded, dtype=out_dtype, device=device)
         outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
-    reducer = HipLocalReducer(ctx, tables[-1], in_dtype, outs, out_dtype, prior_waves=tables[:-1])
+    reducer = HipLocalReducer(ctx, tables[-1], in_dtype, outs, out_dtype, prior_waves=tables[:-1],
+                              use_plan=not args.no_plan)
     local_totals = [float(sum(my_weights))] * T
     global_totals = [float(sum(weights_all))] * T
 
@@ -366,6 +368,7 @@ def main() -> int:
             "clients_per_gpu": n_local,
             "total_clients": n_total,
             "clients_per_launch": wave,
+            "client_table": "re-staged every round" if args.no_plan else "prepared once (persistent client slots)",
             "params_per_client": P,
             "tensors_per_client": T,
             "in_dtype": args.in_dtype,

@@ -757,6 +757,19 @@ struct Staged {
   std::vector<int32_t> kseg;
 };
 
+}  // namespace
+
+struct fedavg_plan {
+  fedavg_ctx* ctx = nullptr;
+  Staged st;
+  char* dev = nullptr;
+  int32_t in_dtype = 0;
+  int out_kind = 0;
+  int split = 1;
+};
+
+namespace {
+
 // Significand width of a weight (bits between its leading and trailing one).
 void note_weight(Staged& st, double w) {
   if (w == 0.0) return;
@@ -788,32 +801,42 @@ bool fma_exact_call(const Staged& st, int32_t in_dtype) {
 }
 
 // Build segment-major compacted tables in a pinned slot and enqueue their H2D copy.
-int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptrs,
-                     const double* weights, int32_t K, void* const* out_ptrs,
-                     const double* wtot, const int32_t* acc_in, Staged& st) {
+// Offsets of the per-call table blob (one allocation, 16-B aligned sections).
+struct BlobLayout {
+  size_t off_ptr, off_w, off_kseg, off_accin, off_outs, off_wtot, bytes;
+  BlobLayout(int T, int Kr) {
+    off_ptr = 0;
+    off_w = align_up(off_ptr + sizeof(void*) * T * Kr, 16);
+    off_kseg = align_up(off_w + sizeof(double) * T * Kr, 16);
+    off_accin = align_up(off_kseg + sizeof(int32_t) * T, 16);
+    off_outs = align_up(off_accin + sizeof(int32_t) * T, 16);
+    off_wtot = align_up(off_outs + sizeof(void*) * T, 16);
+    bytes = align_up(off_wtot + sizeof(double) * T, 256);
+  }
+  void point(char* d, CallTables& tab) const {
+    tab.cptrs = reinterpret_cast<const void* const*>(d + off_ptr);
+    tab.w = reinterpret_cast<const double*>(d + off_w);
+    tab.kseg = reinterpret_cast<const int32_t*>(d + off_kseg);
+    tab.acc_in = reinterpret_cast<const int32_t*>(d + off_accin);
+    tab.outs = reinterpret_cast<void* const*>(d + off_outs);
+    tab.wtot = reinterpret_cast<const double*>(d + off_wtot);
+  }
+};
+
+// Host image of the tables: segment-major compaction of the [K][T] client table.
+void build_blob(const fedavg_ctx* c, const void* const* client_ptrs, const double* weights, int32_t K,
+                void* const* out_ptrs, const double* wtot, const int32_t* acc_in, Staged& st,
+                std::vector<char>& blob, const BlobLayout& L) {
   const int T = c->T;
   const int Kr = std::max(K, 1);
-  const size_t off_ptr = 0;
-  const size_t off_w = align_up(off_ptr + sizeof(void*) * T * Kr, 16);
-  const size_t off_kseg = align_up(off_w + sizeof(double) * T * Kr, 16);
-  const size_t off_accin = align_up(off_kseg + sizeof(int32_t) * T, 16);
-  const size_t off_outs = align_up(off_accin + sizeof(int32_t) * T, 16);
-  const size_t off_wtot = align_up(off_outs + sizeof(void*) * T, 16);
-  const size_t bytes = align_up(off_wtot + sizeof(double) * T, 256);
-
-  // Build the blob in host scratch first: when it is byte-identical to the previous call's
-  // (same clients, weights, outputs — e.g. persistent client slots round after round), the
-  // device copy already holds it and no upload is issued.
-  std::vector<char>& blob = c->scratch;
-  blob.assign(bytes, 0);
+  blob.assign(L.bytes, 0);
   char* h = blob.data();
-  const void** hp = reinterpret_cast<const void**>(h + off_ptr);
-  double* hw = reinterpret_cast<double*>(h + off_w);
-  int32_t* hk = reinterpret_cast<int32_t*>(h + off_kseg);
-  int32_t* ha = reinterpret_cast<int32_t*>(h + off_accin);
-  void** ho = reinterpret_cast<void**>(h + off_outs);
-  double* hwt = reinterpret_cast<double*>(h + off_wtot);
-
+  const void** hp = reinterpret_cast<const void**>(h + L.off_ptr);
+  double* hw = reinterpret_cast<double*>(h + L.off_w);
+  int32_t* hk = reinterpret_cast<int32_t*>(h + L.off_kseg);
+  int32_t* ha = reinterpret_cast<int32_t*>(h + L.off_accin);
+  void** ho = reinterpret_cast<void**>(h + L.off_outs);
+  double* hwt = reinterpret_cast<double*>(h + L.off_wtot);
   st.kseg.assign(T, 0);
   st.stride = Kr;
   st.aligned = true;
@@ -838,6 +861,18 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
     if (out_ptrs && reinterpret_cast<uintptr_t>(out_ptrs[t]) % 16 != 0) st.aligned = false;
     hwt[t] = wtot ? wtot[t] : 1.0;
   }
+}
+
+int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptrs,
+                     const double* weights, int32_t K, void* const* out_ptrs,
+                     const double* wtot, const int32_t* acc_in, Staged& st) {
+  const BlobLayout L(c->T, std::max(K, 1));
+  const size_t bytes = L.bytes;
+  // Build the blob in host scratch first: when it is byte-identical to the previous call's
+  // (same clients, weights, outputs — e.g. persistent client slots round after round), the
+  // device copy already holds it and no upload is issued.
+  std::vector<char>& blob = c->scratch;
+  build_blob(c, client_ptrs, weights, K, out_ptrs, wtot, acc_in, st, blob, L);
 
   char* d = nullptr;
   if (c->last_slot >= 0 && c->last_blob.size() == bytes &&
@@ -868,13 +903,7 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
     c->last_slot = slot;
     d = sl.dev;
   }
-
-  st.tab.cptrs = reinterpret_cast<const void* const*>(d + off_ptr);
-  st.tab.w = reinterpret_cast<const double*>(d + off_w);
-  st.tab.kseg = reinterpret_cast<const int32_t*>(d + off_kseg);
-  st.tab.acc_in = reinterpret_cast<const int32_t*>(d + off_accin);
-  st.tab.outs = reinterpret_cast<void* const*>(d + off_outs);
-  st.tab.wtot = reinterpret_cast<const double*>(d + off_wtot);
+  L.point(d, st.tab);
   return FEDAVG_OK;
 }
 
@@ -1364,6 +1393,70 @@ int32_t fedavg_prof_collect(fedavg_ctx* c, double* total_ms, int32_t* launches) 
     c->event_pool.push_back(pr.second);
   }
   c->prof_events.clear();
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_plan_create(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                           const double* weights, int32_t K, void* const* out_ptrs, int32_t out_dtype,
+                           fedavg_plan** out) {
+  FEDAVG_RET(check_ctx(c));
+  if (!out) return fail(FEDAVG_ERR_INVALID, "null out");
+  *out = nullptr;
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  if (K == 0) return fail(FEDAVG_ERR_STATE, "a plan needs clients");
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (!out_ptrs) return fail(FEDAVG_ERR_INVALID, "null out table");
+  std::vector<double> wtot(c->T, 0.0);
+  std::vector<int32_t> has(c->T, 0);
+  for (int k = 0; k < K; ++k)
+    for (int t = 0; t < c->T; ++t)
+      if (client_ptrs[static_cast<int64_t>(k) * c->T + t] != nullptr) {
+        wtot[t] += weights[static_cast<int64_t>(k) * c->T + t];  // arrival order
+        has[t] = 1;
+      }
+  for (int t = 0; t < c->T; ++t) {
+    if (!has[t]) return fail(FEDAVG_ERR_STATE, "segment " + std::to_string(t) + " has no client data");
+    if (!out_ptrs[t]) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+  }
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  auto* p = new fedavg_plan();
+  p->ctx = c;
+  p->in_dtype = in_dtype;
+  p->out_kind = ok;
+  const BlobLayout L(c->T, K);
+  std::vector<int32_t> no_acc(c->T, 0);
+  std::vector<char> blob;
+  build_blob(c, client_ptrs, weights, K, out_ptrs, wtot.data(), no_acc.data(), p->st, blob, L);
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->dev), L.bytes);
+  if (e == hipSuccess) e = hipMemcpy(p->dev, blob.data(), L.bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (p->dev) (void)hipFree(p->dev);
+    delete p;
+    return fail(FEDAVG_ERR_HIP, std::string("plan upload: ") + hipGetErrorString(e));
+  }
+  L.point(p->dev, p->st.tab);
+  p->split = choose_split(c, p->st.Kmax);
+  *out = p;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_plan_run(fedavg_plan* p, void* stream) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  fedavg_ctx* c = p->ctx;
+  for (int t = 0; t < c->T; ++t)
+    if (c->valid[t]) return fail(FEDAVG_ERR_STATE, "plan run on a context holding accumulated data");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, p->split, 0, 0,
+                     static_cast<int32_t>(c->tiles1.size()));
+}
+
+int32_t fedavg_plan_destroy(fedavg_plan* p) {
+  if (!p) return FEDAVG_OK;
+  if (p->ctx) (void)hipSetDevice(p->ctx->device);
+  (void)hipDeviceSynchronize();
+  if (p->dev) (void)hipFree(p->dev);
+  delete p;
   return FEDAVG_OK;
 }
 

@@ -340,6 +340,24 @@ class FedAvgContext:
             self._lib.fedavg_finalize_range(self._h, ot, out_code(out_dtype), tile_begin, tile_end, self.stream)
         )
 
+    def plan(
+        self, table: ClientTable, in_dtype: torch.dtype, outs: Sequence[torch.Tensor] | OutputTable,
+        out_dtype: torch.dtype,
+    ) -> AggregatePlan:
+        """Prepare ``aggregate(table, in_dtype, outs, out_dtype)`` once; ``plan.run()`` repeats it
+        with no host staging (the table's tensors and the outputs must stay alive)."""
+        self._check_table(table, in_dtype)
+        p, w = table.arrays()
+        ot = self._out_table(outs, out_dtype)
+        h = ctypes.c_void_p()
+        _native.check(
+            self._lib.fedavg_plan_create(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), w.ctypes.data_as(_DBL),
+                table.num_clients, ot, out_code(out_dtype), ctypes.byref(h),
+            )
+        )
+        return AggregatePlan(self, h, keep=(table, outs))
+
     def set_fused_fold(self, enable: bool) -> None:
         """Allow the one-instruction fold when every product is provably exact (default on)."""
         _native.check(self._lib.fedavg_set_fused_fold(self._h, 1 if enable else 0))
@@ -394,6 +412,29 @@ class FedAvgContext:
         ms, n = ctypes.c_double(), ctypes.c_int32()
         _native.check(self._lib.fedavg_prof_collect(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+
+class AggregatePlan:
+    """A prepared fused aggregation (``fedavg_plan_*``)."""
+
+    def __init__(self, ctx: FedAvgContext, handle: ctypes.c_void_p, keep: tuple) -> None:
+        self.ctx = ctx
+        self._h = handle
+        self._keep = keep
+
+    def run(self) -> None:
+        _native.check(self.ctx._lib.fedavg_plan_run(self._h, self.ctx.stream))
+
+    def close(self) -> None:
+        if self._h is not None and self._h.value:
+            self.ctx._lib.fedavg_plan_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self) -> None:  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def bw_probe(src: torch.Tensor, dst: torch.Tensor, mode: int) -> None:

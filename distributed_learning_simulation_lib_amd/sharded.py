@@ -68,8 +68,11 @@ class HipLocalReducer:
         outs: Sequence[torch.Tensor] | OutputTable | None,
         out_dtype: torch.dtype,
         prior_waves: Sequence[ClientTable] = (),
+        use_plan: bool = True,
     ) -> None:
         self.ctx = ctx
+        self.use_plan = use_plan
+        self._plan = None
         self.table = table
         self.in_dtype = in_dtype
         self.outs = outs
@@ -104,6 +107,12 @@ class HipLocalReducer:
     def fused(self) -> None:
         """Single-rank shortcut: fold + divide in the last wave's launch, no extra fp64 pass."""
         assert self.outs is not None
+        if self.use_plan and not self.prior_waves and self.table is not None:
+            # persistent client slots: the table is staged once, each round is one launch
+            if self._plan is None:
+                self._plan = self.ctx.plan(self.table, self.in_dtype, self.outs, self.out_dtype)
+            self._plan.run()
+            return
         self.prefold()
         self.ctx.aggregate(self.table, self.in_dtype, self.outs, self.out_dtype)
 

@@ -169,6 +169,21 @@ int32_t fedavg_finalize_range(fedavg_ctx* ctx, void* const* out_ptrs, int32_t ou
                               int32_t tile_begin, int32_t tile_end, void* stream);
 
 /*
+ * Prepared aggregation ("plan"): the client table, weights and outputs of a
+ * fedavg_aggregate call are validated, compacted and uploaded ONCE; fedavg_plan_run then
+ * launches the fused fold + divide with no host staging (persistent client slots, e.g. a
+ * server that reuses its device buffers round after round). A run is exactly
+ * fedavg_aggregate(ctx, <the planned arguments>) on a context with nothing accumulated.
+ * The buffers named by the plan must outlive it.
+ */
+typedef struct fedavg_plan fedavg_plan;
+int32_t fedavg_plan_create(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                           const double* weights, int32_t num_clients, void* const* out_ptrs,
+                           int32_t out_dtype, fedavg_plan** out);
+int32_t fedavg_plan_run(fedavg_plan* plan, void* stream);
+int32_t fedavg_plan_destroy(fedavg_plan* plan);
+
+/*
  * Synchronise `stream` and report the NaN flag: FEDAVG_OK, FEDAVG_ERR_NAN_ACCUM or
  * FEDAVG_ERR_NAN_RESULT. *flags_out (optional) receives the raw flag bits.
  */

@@ -306,3 +306,28 @@ def test_native_rejects_bad_arguments(hip_device):
     out = [torch.empty(100, dtype=torch.float64, device=hip_device)]
     with pytest.raises(_native.NativeError):  # nothing accumulated (fed_avg_algorithm.py:88)
         ctx.aggregate(None, torch.float32, out, torch.float64)
+
+
+def test_plan_equals_aggregate_and_guards_state(hip_device):
+    rng = np.random.default_rng(21)
+    layout = _random_layout(rng, n_seg=4, max_numel=30000)
+    rows = _clients(layout, 13, torch.float32, hip_device, seed=21)
+    weights = [[float(rng.integers(100, 5000))] * 4 for _ in range(13)]
+    table = ClientTable(4)
+    for r, w in zip(rows, weights):
+        table.add_client(r, w)
+    ctx = FedAvgContext(layout, hip_device)
+    outs = [torch.empty(n, dtype=torch.float32, device=hip_device) for n in layout.numels]
+    plan = ctx.plan(table, torch.float32, outs, torch.float32)
+    for _ in range(3):
+        plan.run()
+        ctx.raise_on_nan()
+        for o, w in zip(outs, _oracle(rows, weights, layout)):
+            assert bits_equal(o.double().cpu().numpy(), w.astype(np.float32).astype(np.float64))
+    t1 = ClientTable(4)
+    t1.add_client(rows[0], weights[0])
+    ctx.accumulate(t1, torch.float32)
+    from distributed_learning_simulation_lib_amd import _native
+    with pytest.raises(_native.NativeError):  # the context holds accumulated data
+        plan.run()
+    plan.close()

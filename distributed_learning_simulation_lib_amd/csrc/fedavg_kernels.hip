@@ -86,6 +86,12 @@ constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
 #ifndef FEDAVG_LOAD_FENCE
 #define FEDAVG_LOAD_FENCE 0
 #endif
+#ifndef FEDAVG_MIN_WAVES  // __launch_bounds__ minimum waves per SIMD (caps VGPRs: 8 -> <= 64)
+#define FEDAVG_MIN_WAVES 1
+#endif
+#ifndef FEDAVG_ABLATE_EPILOGUE
+#define FEDAVG_ABLATE_EPILOGUE 0
+#endif
 #ifndef FEDAVG_NT_STORE
 #define FEDAVG_NT_STORE 1
 #endif
@@ -123,7 +129,7 @@ struct KArgs {
   uint32_t* flag;
   int32_t tile_begin;
   int32_t K;           // row stride of the [T][K] tables
-  int32_t zero_init;   // start every segment at +0.0 (shard partials)
+  int32_t zero_init;   // start every segment at the identity -0.0, ignore acc_in (shard partials)
 };
 
 enum OutKind : int { OUT_ACC = 0, OUT_F32 = 1, OUT_F64 = 2 };
@@ -369,42 +375,40 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     return to_global<T>(reinterpret_cast<const void*>(cp[k] + elem_off));
   };
 
-  double acc[kAE] = {};
-  bool have = false;  // wave-uniform
-  if (SPLIT == 1 || wave == 0) {
-    if (a.zero_init) {
+  // The accumulator starts at -0.0, the additive identity of IEEE addition: -0.0 + p == p
+  // for every p (including -0.0 and +0.0), and fma(x, w, -0.0) == round(x * w). Folding the
+  // first client into it therefore equals the reference's assignment `acc = tmp`
+  // (fed_avg_algorithm.py:55-56) bit for bit, signed zeros included, with no special case.
+  double acc[kAE];
 #pragma unroll
-      for (int i = 0; i < kAE; ++i) acc[i] = 0.0;
-      have = true;
-    } else if (to_const<int32_t>(a.tab.acc_in)[seg]) {
-      const gptr<const double> ap = to_global<double>(a.acc + acc_base);
+  for (int i = 0; i < kAE; ++i) acc[i] = -0.0;
+  bool have = a.zero_init != 0;  // wave-uniform: "this wave holds a value for the tile"
+  if ((SPLIT == 1 || wave == 0) && !a.zero_init && to_const<int32_t>(a.tab.acc_in)[seg]) {
+    const gptr<const double> ap = to_global<double>(a.acc + acc_base);
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        const int e = (v * LANES + li) * N;
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
 #pragma unroll
-        for (int j = 0; j < N; j += 2) {
-          if (FULL || e + j + 2 <= count) {
-            const f64x2 d = *(gptr<const f64x2>)(ap + e + j);
-            acc[v * N + j] = d.x;
-            acc[v * N + j + 1] = d.y;
-          } else {
-            acc[v * N + j] = (e + j < count) ? ap[e + j] : 0.0;
-            acc[v * N + j + 1] = (e + j + 1 < count) ? ap[e + j + 1] : 0.0;
-          }
+      for (int j = 0; j < N; j += 2) {
+        if (FULL || e + j + 2 <= count) {
+          const f64x2 d = *(gptr<const f64x2>)(ap + e + j);
+          acc[v * N + j] = d.x;
+          acc[v * N + j + 1] = d.y;
+        } else {
+          if (e + j < count) acc[v * N + j] = ap[e + j];
+          if (e + j + 1 < count) acc[v * N + j + 1] = ap[e + j + 1];
         }
       }
-      have = true;
     }
+    have = true;
   }
 
   // Fold this wave's clients [kb, ke) in order, in groups of CU_LOADS clients: all loads of
-  // a group are issued before any is consumed. Group variants are compile-time: FIRST (the
-  // group's first client is an assignment, fed_avg_algorithm.py:55-56) and TAIL (a short last
-  // group: missing slots re-load the group's last client — L2 hits — and are masked out of
-  // the fold by selects, never by branches, so the compiler keeps every load in flight).
+  // a group are issued before any is consumed. A short last group (TAIL) re-loads its last
+  // client for the missing slots (L2 hits) and masks them out of the fold with selects —
+  // never with branches, which made hipcc serialise the loads.
   if constexpr (FAST) {
-    auto group = [&](auto first_tag, auto tail_tag, int k, int n) {
-      constexpr bool FIRST = decltype(first_tag)::value;
+    auto group = [&](auto tail_tag, int k, int n) {
       constexpr bool TAIL = decltype(tail_tag)::value;
       V buf[CU_LOADS][VPL];
       double wk[CU_LOADS];
@@ -426,7 +430,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
           for (int j = 0; j < N; ++j) {
             double& r = acc[v * N + j];
-            const double nv = (FIRST && c == 0) ? x[j] * wk[c] : fold<FMA>(r, x[j], wk[c]);
+            const double nv = fold<FMA>(r, x[j], wk[c]);
             if constexpr (TAIL) {
               r = (c < n) ? nv : r;
             } else {
@@ -436,29 +440,16 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
         }
       }
     };
-    using T1 = std::true_type;
-    using F0 = std::false_type;
     int k = kb;
-    if (!have && k < ke) {
-      if (ke - k >= CU_LOADS) {
-        group(T1{}, F0{}, k, CU_LOADS);
-        k += CU_LOADS;
-      } else {
-        group(T1{}, T1{}, k, ke - k);
-        k = ke;
-      }
-    }
-    for (; k + CU_LOADS <= ke; k += CU_LOADS) group(F0{}, F0{}, k, CU_LOADS);
-    if (k < ke) group(F0{}, T1{}, k, ke - k);
+    for (; k + CU_LOADS <= ke; k += CU_LOADS) group(std::false_type{}, k, CU_LOADS);
+    if (k < ke) group(std::true_type{}, k, ke - k);
   } else {
-    bool first = !have;
     for (int k = kb; k < ke; ++k) {
       const double wk = wp[k];
       double x[kAE];
       LL::load_checked(client(k), li, count, x);
 #pragma unroll
-      for (int i = 0; i < kAE; ++i) acc[i] = first ? x[i] * wk : fold<FMA>(acc[i], x[i], wk);
-      first = false;
+      for (int i = 0; i < kAE; ++i) acc[i] = fold<FMA>(acc[i], x[i], wk);
     }
   }
   have = have || (ke > kb);
@@ -499,7 +490,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const bool in_range = FULL || (e + j < count);
-      bad_acc |= in_range && (acc[v * N + j] != acc[v * N + j]);
+      bad_acc |= in_range && (acc[v * N + j] != acc[v * N + j]) && !FEDAVG_ABLATE_EPILOGUE;
     }
   }
 
@@ -525,14 +516,20 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     bool bad_res = false;
     double res[kAE];
 #pragma unroll
-    for (int i = 0; i < kAE; ++i) res[i] = acc[i] / W;
+    for (int i = 0; i < kAE; ++i) {
+#if FEDAVG_ABLATE_EPILOGUE  // timing-only build: reciprocal multiply, no NaN checks (wrong results)
+      res[i] = acc[i] * (1.0 / W);
+#else
+      res[i] = acc[i] / W;
+#endif
+    }
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int e = (v * LANES + li) * N;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         const bool in_range = FULL || (e + j < count);
-        bad_res |= in_range && (res[v * N + j] != res[v * N + j]);
+        bad_res |= in_range && (res[v * N + j] != res[v * N + j]) && !FEDAVG_ABLATE_EPILOGUE;
       }
     }
     void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
@@ -590,7 +587,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 }
 
 template <typename T, int OUT, int SPLIT, bool VEC, bool FMA>
-__global__ __launch_bounds__((SPLIT == 1) ? kThreads1 : kThreads) void fedavg_tile_kernel(KArgs a) {
+__global__ __launch_bounds__((SPLIT == 1) ? kThreads1 : kThreads, FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
   const TileDesc td = load_tile(a.tiles, a.tile_begin + blockIdx.x);
   constexpr int TILE = ((SPLIT == 1) ? kThreads1 : kThreads / SPLIT) * kAE;

@@ -150,7 +150,8 @@ int32_t fedavg_weighted_avg(fedavg_ctx* ctx, const void* const* client_ptrs, int
  * sum_k w_k x_k, fp64, written to the accumulator (no division). Used by the sharded
  * driver that reduces the per-GPU partials with RCCL and then calls fedavg_aggregate
  * with num_clients = 0 on the root. tile_end = -1 means "all tiles". zero_init != 0 starts
- * every segment at +0.0 (so a shard without clients contributes exact zeros).
+ * every segment at the additive identity -0.0 (so the shard's fold is exact, and a shard
+ * without clients contributes identities).
  */
 int32_t fedavg_partial(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
                        const double* weights, int32_t num_clients, int32_t zero_init,

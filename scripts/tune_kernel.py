@@ -13,11 +13,10 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "ntst": {"FEDAVG_NT_STORE": 1},
-    "ae16_cu512": {"FEDAVG_AE": 16, "FEDAVG_CU_BYTES": 512},
-    "ae16_cu512_ntst": {"FEDAVG_AE": 16, "FEDAVG_CU_BYTES": 512, "FEDAVG_NT_STORE": 1},
-    "t512": {"FEDAVG_THREADS1": 512},
-    "t512_ntst": {"FEDAVG_THREADS1": 512, "FEDAVG_NT_STORE": 1},
+    "w8": {"FEDAVG_MIN_WAVES": 8},
+    "w6": {"FEDAVG_MIN_WAVES": 6},
+    "w8_cu128": {"FEDAVG_MIN_WAVES": 8, "FEDAVG_CU_BYTES": 128},
+    "w4_ae16": {"FEDAVG_MIN_WAVES": 4, "FEDAVG_AE": 16},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 
@@ -61,7 +60,8 @@ def run_all(rounds=7, iters=10):
         torch.cuda.synchronize()
         if ref is None:
             ref = flat.clone()
-        assert torch.equal(ref.view(torch.int32), flat.view(torch.int32)), name
+        if not name.startswith("abl"):
+            assert torch.equal(ref.view(torch.int32), flat.view(torch.int32)), name
     times = {n: [] for n in ctxs}
     for _ in range(rounds):
         for name, ctx in ctxs.items():

@@ -7,7 +7,8 @@ Same plugin surface as ``FedAVGAlgorithm`` in the reference
 ``aggregate_worker_data`` with the same message semantics.
 
 What differs is where the arithmetic happens. ``_accumulate_parameter`` stages each client
-tensor (moving it to the GPU if it arrived in host memory) instead of doing
+tensor (a client that arrived in host memory is packed into pinned memory and DMA'd to HBM in
+one transfer, ``ingest.py``) instead of doing
 ``acc += x.to(float64) * w`` on the CPU. Every ``wave_size`` clients the wave is folded into a
 device-resident fp64 accumulator by one HIP kernel launch, in arrival order, with separately
 rounded products and sums — bit-identical to the reference's fp64 sequence. The last wave is
@@ -31,6 +32,7 @@ from typing import Any
 import torch
 
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError
+from ..ingest import HostIngest
 from ..message import Message, ModelParameter, ParameterMessage
 from .aggregation_algorithm import (
     AggregationAlgorithm,
@@ -68,6 +70,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__table_dtype: torch.dtype | None = None
         self.__row: dict[str, tuple[torch.Tensor, Any]] = {}
         self.__has_data = False
+        self.__ingest: HostIngest | None = None
 
     # ---- setup -------------------------------------------------------------------------
     @property
@@ -121,7 +124,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if not self.accumulate:
             return
         weight = self._get_weight(worker_data=worker_data, name=name, parameter=parameter)
-        self.__row[name] = (to_device_operand(parameter, self.device), weight)
+        # host tensors are packed and DMA'd per client in _stage_client (ingest.HostIngest)
+        self.__row[name] = (parameter, weight)
         # release to reduce memory pressure (fed_avg_algorithm.py:63-64)
         worker_data.parameter = {}
 
@@ -162,6 +166,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             else:
                 tensors.append(None)
                 weights.append(0.0)
+        tensors = self._to_device_row(tensors)
         present = [t for t in tensors if t is not None]
         if present:
             unified, dt = unify_dtype(present)
@@ -178,6 +183,27 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__has_data = True
         if self.__table.num_clients >= self.wave_size:
             self._flush()
+
+    def _to_device_row(self, tensors: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
+        """One client's tensors in HBM. Host tensors of one kernel dtype go through the pinned
+        ingest (one packed DMA per client); anything else moves tensor by tensor."""
+        host = [t for t in tensors if t is not None and t.device.type == "cpu"]
+        if not host:
+            return [None if t is None else to_device_operand(t, self.device) for t in tensors]
+        dtypes = {t.dtype for t in host}
+        if len(dtypes) == 1 and next(iter(dtypes)) in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
+            if self.__ingest is None:
+                self.__ingest = HostIngest(self.device)
+            assert self.__native_layout is not None
+            moved = self.__ingest.to_device(
+                self.__native_layout, [t if t is not None and t.device.type == "cpu" else None for t in tensors],
+                next(iter(dtypes)),
+            )
+            return [
+                None if t is None else (m if m is not None else to_device_operand(t, self.device))
+                for t, m in zip(tensors, moved)
+            ]
+        return [None if t is None else to_device_operand(t, self.device) for t in tensors]
 
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""

@@ -51,6 +51,11 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
         c_int32,
         [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_int32, c_void_p],
     ),
+    "fedavg_accumulate_delta": (c_int32, [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_void_p]),
+    "fedavg_aggregate_delta": (
+        c_int32,
+        [c_void_p, _PP, c_int32, _PD, c_int32, _PP, _PP, c_int32, c_void_p],
+    ),
     "fedavg_weighted_avg": (
         c_int32,
         [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_int32, c_void_p],

@@ -31,9 +31,9 @@ from typing import Any
 
 import torch
 
-from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError
+from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
-from ..message import Message, ModelParameter, ParameterMessage
+from ..message import DeltaParameterMessage, Message, ModelParameter, ParameterMessage
 from .aggregation_algorithm import (
     AggregationAlgorithm,
     default_device,
@@ -68,6 +68,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__ctx_key: tuple | None = None
         self.__table: ClientTable | None = None
         self.__table_dtype: torch.dtype | None = None
+        self.__table_delta = False
+        self.__base: OutputTable | None = None
         self.__row: dict[str, tuple[torch.Tensor, Any]] = {}
         self.__has_data = False
         self.__ingest: HostIngest | None = None
@@ -105,6 +107,19 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_data = self._all_worker_data.get(worker_id, None)
         if worker_data is None:
             return True
+        if isinstance(worker_data, DeltaParameterMessage) and self.accumulate and self._delta_fusable(worker_data):
+            # restore() fused into the fold: x = old + delta in the kernel (message.py:40-61)
+            assert self._old_parameter is not None
+            assert len(worker_data.delta_parameter) == len(self._old_parameter)
+            if self.__layout is None:
+                self._set_layout(self._old_parameter)
+            self.__row = {}
+            for name, delta in worker_data.delta_parameter.items():
+                weight = self._get_weight(worker_data=worker_data, name=name, parameter=delta)
+                self.__row[name] = (delta, weight)
+            worker_data.delta_parameter = {}
+            self._stage_client(delta=True)
+            return True
         if not isinstance(worker_data, ParameterMessage):
             return True
         self.__row = {}
@@ -113,6 +128,29 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if self.accumulate:
             self._stage_client()
         return True
+
+    # The server hands DeltaParameterMessages straight to this algorithm (with the cached global
+    # model set through set_old_parameter) instead of restoring them on the host first.
+    accepts_delta_messages = True
+
+    def _delta_fusable(self, msg: DeltaParameterMessage) -> bool:
+        # the consistency-check fields of restore() (message.py:42-59) need the host path
+        return self._old_parameter is not None and msg.old_parameter is None and msg.new_parameter is None
+
+    def set_old_parameter(self, old_parameter: ModelParameter) -> None:
+        if old_parameter is not self._old_parameter:
+            self.__base = None
+        super().set_old_parameter(old_parameter)
+
+    def _delta_base(self) -> OutputTable:
+        """The cached global model as fp64 device tensors in native-layout order."""
+        if self.__base is None:
+            assert self._old_parameter is not None and self.__native_layout is not None and self.__layout is not None
+            names = [self.__layout.names[i] for i in self.__keep]
+            tensors = [self._old_parameter[n].to(device=self.device, dtype=torch.float64).contiguous().view(-1)
+                       for n in names]
+            self.__base = OutputTable(tensors, self.__native_layout, self.device, torch.float64)
+        return self.__base
 
     def _accumulate_parameter(
         self,
@@ -135,7 +173,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _apply_total_weight(self, name: str, parameter: torch.Tensor, total_weight: Any) -> torch.Tensor:
         return parameter / total_weight
 
-    def _stage_client(self) -> None:
+    def _stage_client(self, delta: bool = False) -> None:
         row = self.__row
         self.__row = {}
         if not row:
@@ -174,11 +212,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             tensors = [next(it) if t is not None else None for t in tensors]
         else:
             dt = self.__table_dtype or torch.float32
-        if self.__table is not None and self.__table_dtype != dt:
+        if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
             self._flush()
         if self.__table is None:
             self.__table = ClientTable(len(self.__keep))
             self.__table_dtype = dt
+            self.__table_delta = delta
         self.__table.add_client(tensors, weights)
         self.__has_data = True
         if self.__table.num_clients >= self.wave_size:
@@ -213,7 +252,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         table, dt = self.__table, self.__table_dtype
         assert dt is not None
         self.__table, self.__table_dtype = None, None
-        ctx.accumulate(table, dt)
+        if self.__table_delta:
+            ctx.accumulate_delta(table, dt, self._delta_base())
+        else:
+            ctx.accumulate(table, dt)
 
     # ---- end of round (fed_avg_algorithm.py:76-113) ------------------------------------
     def _aggregate_parameter(self, chosen_worker_ids: set[int] | None = None) -> ModelParameter:
@@ -254,14 +296,21 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                            dtype=out_dtype, device=self.device)
         offs, _ = native.padded_offsets(flat.element_size())
         outs = [flat[o : o + n] for o, n in zip(offs, native.numels)]
+        delta = self.__table_delta and table is not None
         try:
             if not custom_divide:
-                ctx.aggregate(table, dt or torch.float32, outs, out_dtype)
+                if delta:
+                    ctx.aggregate_delta(table, dt, self._delta_base(), outs, out_dtype)
+                else:
+                    ctx.aggregate(table, dt or torch.float32, outs, out_dtype)
                 ctx.raise_on_nan(pending)
             else:
                 # a subclass divides: finalize with a unit divisor (exact), then call its hook
                 if table is not None and dt is not None:
-                    ctx.accumulate(table, dt)
+                    if delta:
+                        ctx.accumulate_delta(table, dt, self._delta_base())
+                    else:
+                        ctx.accumulate(table, dt)
                 totals = ctx.total_weights()
                 ctx.set_accumulated([1.0] * native.num_segments)
                 ctx.finalize_range(outs, torch.float64)

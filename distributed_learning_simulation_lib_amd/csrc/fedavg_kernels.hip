@@ -119,6 +119,7 @@ struct CallTables {
   const int32_t* acc_in;     // [T] 1 = accumulator holds data for the segment
   void* const* outs;         // [T] output pointers (final kernels)
   const double* wtot;        // [T] divisor (final kernels)
+  const void* const* base;   // [T] fp64 base model (delta calls): x = base + delta
 };
 
 struct KArgs {
@@ -334,17 +335,27 @@ __device__ __forceinline__ void store_out(gptr<V> p, V v) {
 // exact in fp64 (FMA = true: the weight's significand fits beside the input's, e.g. integer
 // dataset sizes and fp32 inputs), round(acc + x*w) == fma(x, w, acc) and one instruction does
 // it; otherwise the two roundings are kept.
-template <bool FMA>
-__device__ __forceinline__ double fold(double acc, double x, double w) {
-  if constexpr (FMA) {
+//
+// FOLD_DELTA: the client sent a delta against the server's global model
+// (DeltaParameterMessage.restore, message.py:40-61): x = base + delta in fp64 (rounded, like
+// `old.to(float64) + v`), then the separately rounded product and sum.
+enum FoldKind : int { FOLD_MULADD = 0, FOLD_FMA = 1, FOLD_DELTA = 2 };
+
+template <int FOLD>
+__device__ __forceinline__ double fold(double acc, double x, double w, double base) {
+  if constexpr (FOLD == FOLD_FMA) {
     return __builtin_fma(x, w, acc);
+  } else if constexpr (FOLD == FOLD_DELTA) {
+    const double full = base + x;
+    const double p = full * w;
+    return acc + p;
   } else {
     const double p = x * w;
     return acc + p;
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, bool FMA>
+template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD>
 __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
   constexpr int LANES = (SPLIT == 1) ? kThreads1 : kThreads / SPLIT;  // lanes sharing one client stream
   using LL = LaneLoader<T, LANES, FULL && VEC, VEC>;
@@ -403,6 +414,31 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     have = true;
   }
 
+  // delta calls: the base model's slice of this tile, fp64, read once per tile (L2-shared
+  // by nothing else: one read of the base per fold, like one more client)
+  double base[kAE];
+#pragma unroll
+  for (int i = 0; i < kAE; ++i) base[i] = 0.0;
+  if constexpr (FOLD == FOLD_DELTA) {
+    const gptr<const double> bp =
+        to_global<double>(reinterpret_cast<const void*>(to_const<uint64_t>(a.tab.base)[seg])) + td.start;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+#pragma unroll
+      for (int j = 0; j < N; j += 2) {
+        if (VEC && (FULL || e + j + 2 <= count)) {
+          const f64x2 d = *(gptr<const f64x2>)(bp + e + j);
+          base[v * N + j] = d.x;
+          base[v * N + j + 1] = d.y;
+        } else {
+          if (e + j < count) base[v * N + j] = bp[e + j];
+          if (e + j + 1 < count) base[v * N + j + 1] = bp[e + j + 1];
+        }
+      }
+    }
+  }
+
   // Fold this wave's clients [kb, ke) in order, in groups of CU_LOADS clients: all loads of
   // a group are issued before any is consumed. A short last group (TAIL) re-loads its last
   // client for the missing slots (L2 hits) and masks them out of the fold with selects —
@@ -430,7 +466,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
           for (int j = 0; j < N; ++j) {
             double& r = acc[v * N + j];
-            const double nv = fold<FMA>(r, x[j], wk[c]);
+            const double nv = fold<FOLD>(r, x[j], wk[c], base[v * N + j]);
             if constexpr (TAIL) {
               r = (c < n) ? nv : r;
             } else {
@@ -449,7 +485,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
       double x[kAE];
       LL::load_checked(client(k), li, count, x);
 #pragma unroll
-      for (int i = 0; i < kAE; ++i) acc[i] = fold<FMA>(acc[i], x[i], wk);
+      for (int i = 0; i < kAE; ++i) acc[i] = fold<FOLD>(acc[i], x[i], wk, base[i]);
     }
   }
   have = have || (ke > kb);
@@ -586,15 +622,15 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC, bool FMA>
+template <typename T, int OUT, int SPLIT, bool VEC, int FOLD>
 __global__ __launch_bounds__((SPLIT == 1) ? kThreads1 : kThreads, FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
   const TileDesc td = load_tile(a.tiles, a.tile_begin + blockIdx.x);
   constexpr int TILE = ((SPLIT == 1) ? kThreads1 : kThreads / SPLIT) * kAE;
   if (td.count == TILE) {
-    tile_body<T, OUT, SPLIT, VEC, true, FMA>(a, td, lds);
+    tile_body<T, OUT, SPLIT, VEC, true, FOLD>(a, td, lds);
   } else {
-    tile_body<T, OUT, SPLIT, VEC, false, FMA>(a, td, lds);
+    tile_body<T, OUT, SPLIT, VEC, false, FOLD>(a, td, lds);
   }
 }
 
@@ -749,6 +785,7 @@ struct Staged {
   int32_t Kmax = 0;
   int32_t stride = 1;    // row stride of the [T][K] tables
   bool aligned = true;
+  bool delta = false;           // clients are deltas against tab.base (fp64)
   int32_t max_weight_bits = 0;  // largest significand (bits) among the call's weights
   bool weights_tame = true;     // every weight finite, zero or within [2^-800, 2^800]   // every client/out pointer is 16-byte aligned
   std::vector<int32_t> kseg;
@@ -800,7 +837,7 @@ bool fma_exact_call(const Staged& st, int32_t in_dtype) {
 // Build segment-major compacted tables in a pinned slot and enqueue their H2D copy.
 // Offsets of the per-call table blob (one allocation, 16-B aligned sections).
 struct BlobLayout {
-  size_t off_ptr, off_w, off_kseg, off_accin, off_outs, off_wtot, bytes;
+  size_t off_ptr, off_w, off_kseg, off_accin, off_outs, off_wtot, off_base, bytes;
   BlobLayout(int T, int Kr) {
     off_ptr = 0;
     off_w = align_up(off_ptr + sizeof(void*) * T * Kr, 16);
@@ -808,7 +845,8 @@ struct BlobLayout {
     off_accin = align_up(off_kseg + sizeof(int32_t) * T, 16);
     off_outs = align_up(off_accin + sizeof(int32_t) * T, 16);
     off_wtot = align_up(off_outs + sizeof(void*) * T, 16);
-    bytes = align_up(off_wtot + sizeof(double) * T, 256);
+    off_base = align_up(off_wtot + sizeof(double) * T, 16);
+    bytes = align_up(off_base + sizeof(void*) * T, 256);
   }
   void point(char* d, CallTables& tab) const {
     tab.cptrs = reinterpret_cast<const void* const*>(d + off_ptr);
@@ -817,13 +855,14 @@ struct BlobLayout {
     tab.acc_in = reinterpret_cast<const int32_t*>(d + off_accin);
     tab.outs = reinterpret_cast<void* const*>(d + off_outs);
     tab.wtot = reinterpret_cast<const double*>(d + off_wtot);
+    tab.base = reinterpret_cast<const void* const*>(d + off_base);
   }
 };
 
 // Host image of the tables: segment-major compaction of the [K][T] client table.
 void build_blob(const fedavg_ctx* c, const void* const* client_ptrs, const double* weights, int32_t K,
                 void* const* out_ptrs, const double* wtot, const int32_t* acc_in, Staged& st,
-                std::vector<char>& blob, const BlobLayout& L) {
+                std::vector<char>& blob, const BlobLayout& L, const void* const* base_ptrs = nullptr) {
   const int T = c->T;
   const int Kr = std::max(K, 1);
   blob.assign(L.bytes, 0);
@@ -834,6 +873,8 @@ void build_blob(const fedavg_ctx* c, const void* const* client_ptrs, const doubl
   int32_t* ha = reinterpret_cast<int32_t*>(h + L.off_accin);
   void** ho = reinterpret_cast<void**>(h + L.off_outs);
   double* hwt = reinterpret_cast<double*>(h + L.off_wtot);
+  const void** hb = reinterpret_cast<const void**>(h + L.off_base);
+  st.delta = base_ptrs != nullptr;
   st.kseg.assign(T, 0);
   st.stride = Kr;
   st.aligned = true;
@@ -857,19 +898,22 @@ void build_blob(const fedavg_ctx* c, const void* const* client_ptrs, const doubl
     ho[t] = out_ptrs ? out_ptrs[t] : nullptr;
     if (out_ptrs && reinterpret_cast<uintptr_t>(out_ptrs[t]) % 16 != 0) st.aligned = false;
     hwt[t] = wtot ? wtot[t] : 1.0;
+    hb[t] = base_ptrs ? base_ptrs[t] : nullptr;
+    if (base_ptrs && reinterpret_cast<uintptr_t>(base_ptrs[t]) % 16 != 0) st.aligned = false;
   }
 }
 
 int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptrs,
                      const double* weights, int32_t K, void* const* out_ptrs,
-                     const double* wtot, const int32_t* acc_in, Staged& st) {
+                     const double* wtot, const int32_t* acc_in, Staged& st,
+                     const void* const* base_ptrs = nullptr) {
   const BlobLayout L(c->T, std::max(K, 1));
   const size_t bytes = L.bytes;
   // Build the blob in host scratch first: when it is byte-identical to the previous call's
   // (same clients, weights, outputs — e.g. persistent client slots round after round), the
   // device copy already holds it and no upload is issued.
   std::vector<char>& blob = c->scratch;
-  build_blob(c, client_ptrs, weights, K, out_ptrs, wtot, acc_in, st, blob, L);
+  build_blob(c, client_ptrs, weights, K, out_ptrs, wtot, acc_in, st, blob, L, base_ptrs);
 
   char* d = nullptr;
   if (c->last_slot >= 0 && c->last_blob.size() == bytes &&
@@ -905,28 +949,37 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
 }
 
 template <typename T, int OUT, int SPLIT, bool VEC>
-hipError_t launch_fma(const KArgs& a, bool fma, int nblocks, hipStream_t s) {
+hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s) {
   const int threads = (SPLIT == 1) ? kThreads1 : kThreads;
-  if (fma) hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, true>), dim3(nblocks), dim3(threads), 0, s, a);
-  else hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, false>), dim3(nblocks), dim3(threads), 0, s, a);
+  if (fold == FOLD_FMA) {
+    hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA>), dim3(nblocks), dim3(threads), 0, s, a);
+  } else if (fold == FOLD_DELTA) {
+    if constexpr (SPLIT == 1) {
+      hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA>), dim3(nblocks), dim3(threads), 0, s, a);
+    } else {
+      return hipErrorInvalidValue;  // delta calls run the exact-order kernel only
+    }
+  } else {
+    hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD>), dim3(nblocks), dim3(threads), 0, s, a);
+  }
   return hipGetLastError();
 }
 
 template <typename T, int OUT>
-hipError_t launch_typed(const KArgs& a, int split, bool vec, bool fma, int nblocks, hipStream_t s) {
+hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s) {
   if (split == 4) {
-    return vec ? launch_fma<T, OUT, 4, true>(a, fma, nblocks, s) : launch_fma<T, OUT, 4, false>(a, fma, nblocks, s);
+    return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s) : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s);
   }
-  return vec ? launch_fma<T, OUT, 1, true>(a, fma, nblocks, s) : launch_fma<T, OUT, 1, false>(a, fma, nblocks, s);
+  return vec ? launch_fold<T, OUT, 1, true>(a, fold, nblocks, s) : launch_fold<T, OUT, 1, false>(a, fold, nblocks, s);
 }
 
 template <int OUT>
-hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, bool fma, int nblocks, hipStream_t s) {
+hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s) {
   switch (in_dtype) {
-    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fma, nblocks, s);
-    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fma, nblocks, s);
-    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fma, nblocks, s);
-    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fma, nblocks, s);
+    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s);
+    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s);
+    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s);
+    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -943,6 +996,7 @@ int choose_split(const fedavg_ctx* c, int kmax) {
 // Launch the main kernel over tiles [tb, te) of the split-specific tile table.
 int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_dtype, int out_kind,
                     int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1) {
+  if (st.delta) split = 1;  // delta folds run the exact-order kernel only
   KArgs a;
   a.segs = c->d_segs;
   a.tab = st.tab;
@@ -972,11 +1026,12 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     FEDAVG_HIP_TRY(hipEventRecord(e0, s));
   }
   hipError_t err = hipSuccess;
-  const bool fma = c->allow_fma && fma_exact_call(st, in_dtype);
+  const int fold = st.delta ? FOLD_DELTA
+                            : (c->allow_fma && fma_exact_call(st, in_dtype)) ? FOLD_FMA : FOLD_MULADD;
   switch (out_kind) {
-    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fma, nblocks, s); break;
-    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fma, nblocks, s); break;
-    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fma, nblocks, s); break;
+    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s); break;
+    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s); break;
+    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s); break;
     default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
   }
   if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
@@ -1214,6 +1269,65 @@ int32_t fedavg_aggregate(fedavg_ctx* c, const void* const* client_ptrs, int32_t 
   FEDAVG_RET(launch_main(c, s, st, K > 0 ? in_dtype : FEDAVG_F32, ok, split, 0, 0,
                          static_cast<int32_t>(c->tiles1.size())));
   // _aggregate_parameter resets the accumulator (fed_avg_algorithm.py:90,98)
+  std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
+  std::fill(c->valid.begin(), c->valid.end(), 0);
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_accumulate_delta(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                                const double* weights, int32_t K, const void* const* base_ptrs,
+                                void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  if (!base_ptrs) return fail(FEDAVG_ERR_INVALID, "null base table");
+  for (int t = 0; t < c->T; ++t)
+    if (!base_ptrs[t]) return fail(FEDAVG_ERR_INVALID, "null base pointer");
+  if (K == 0) return FEDAVG_OK;
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, client_ptrs, weights, K, nullptr, nullptr, c->valid.data(), st, base_ptrs));
+  FEDAVG_RET(launch_main(c, s, st, in_dtype, OUT_ACC, 1, 0, 0, static_cast<int32_t>(c->tiles1.size())));
+  for (int k = 0; k < K; ++k)
+    for (int t = 0; t < c->T; ++t)
+      if (client_ptrs[static_cast<int64_t>(k) * c->T + t] != nullptr) {
+        c->wsum[t] += weights[static_cast<int64_t>(k) * c->T + t];
+        c->valid[t] = 1;
+      }
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_aggregate_delta(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                               const double* weights, int32_t K, const void* const* base_ptrs,
+                               void* const* out_ptrs, int32_t out_dtype, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  if (!base_ptrs) return fail(FEDAVG_ERR_INVALID, "null base table");
+  for (int t = 0; t < c->T; ++t)
+    if (!base_ptrs[t]) return fail(FEDAVG_ERR_INVALID, "null base pointer");
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (out_ptrs == nullptr) return fail(FEDAVG_ERR_INVALID, "null out table");
+  std::vector<double> wtot(c->wsum);
+  std::vector<int32_t> will_have(c->valid);
+  for (int k = 0; k < K; ++k)
+    for (int t = 0; t < c->T; ++t)
+      if (client_ptrs[static_cast<int64_t>(k) * c->T + t] != nullptr) {
+        wtot[t] += weights[static_cast<int64_t>(k) * c->T + t];
+        will_have[t] = 1;
+      }
+  for (int t = 0; t < c->T; ++t) {
+    if (!will_have[t])
+      return fail(FEDAVG_ERR_STATE, "segment " + std::to_string(t) + " has no accumulated data");
+    if (out_ptrs[t] == nullptr) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+  }
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Staged st;
+  FEDAVG_RET(stage_tables(c, s, K > 0 ? client_ptrs : nullptr, weights, K, out_ptrs, wtot.data(),
+                          c->valid.data(), st, base_ptrs));
+  FEDAVG_RET(launch_main(c, s, st, K > 0 ? in_dtype : FEDAVG_F32, ok, 1, 0, 0,
+                         static_cast<int32_t>(c->tiles1.size())));
   std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
   return FEDAVG_OK;

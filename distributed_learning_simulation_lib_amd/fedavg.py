@@ -292,6 +292,39 @@ class FedAvgContext:
             )
         )
 
+    def _base_table(self, base: Sequence[torch.Tensor] | OutputTable) -> ctypes.Array:
+        return self._out_table(base, torch.float64)
+
+    def accumulate_delta(self, table: ClientTable, in_dtype: torch.dtype,
+                         base: Sequence[torch.Tensor] | OutputTable) -> None:
+        """Fold a wave of DELTA clients: x = base + delta (fp64), message.py:40-61 fused."""
+        self._check_table(table, in_dtype)
+        if table.num_clients == 0:
+            return
+        p, w = table.arrays()
+        bt = self._base_table(base)
+        _native.check(
+            self._lib.fedavg_accumulate_delta(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), w.ctypes.data_as(_DBL),
+                table.num_clients, bt, self.stream,
+            )
+        )
+
+    def aggregate_delta(self, table: ClientTable, in_dtype: torch.dtype,
+                        base: Sequence[torch.Tensor] | OutputTable,
+                        outs: Sequence[torch.Tensor] | OutputTable, out_dtype: torch.dtype) -> None:
+        """Last wave of delta clients + divide (fedavg_aggregate with the restore fused)."""
+        self._check_table(table, in_dtype)
+        p, w = table.arrays()
+        bt = self._base_table(base)
+        ot = self._out_table(outs, out_dtype)
+        _native.check(
+            self._lib.fedavg_aggregate_delta(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), w.ctypes.data_as(_DBL),
+                table.num_clients, bt, ot, out_code(out_dtype), self.stream,
+            )
+        )
+
     def weighted_avg(
         self, table: ClientTable, in_dtype: torch.dtype, outs: Sequence[torch.Tensor], out_dtype: torch.dtype
     ) -> None:

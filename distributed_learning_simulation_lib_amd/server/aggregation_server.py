@@ -132,7 +132,11 @@ class AggregationServer:
             old_parameter = self._model_cache.parameter
             if isinstance(data, DeltaParameterMessage):
                 assert old_parameter is not None
-                data = data.restore(old_parameter)
+                if getattr(self._algorithm, "accepts_delta_messages", False):
+                    # the algorithm fuses restore() into its fold (fedavg_*_delta)
+                    self._algorithm.set_old_parameter(old_parameter)
+                else:
+                    data = data.restore(old_parameter)
             elif isinstance(data, ParameterMessage):
                 if old_parameter is not None:
                     data.complete(old_parameter)

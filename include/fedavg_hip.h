@@ -13,6 +13,8 @@
  *                           simulation_lib/algorithm/aggregation_algorithm.py:51-76
  *   fedavg_partial       <- the per-shard half of _accumulate_parameter when clients are
  *                           sharded across GPUs (fp64 partial sum, no division)
+ *   fedavg_*_delta       <- DeltaParameterMessage.restore fused into the fold (message.py:40-61,
+ *                           aggregation_server.py:121-125)
  *   fedavg_check         <- the NaN assertions fed_avg_algorithm.py:35,93,97
  *   fedavg_find_nan_clients <- which client tripped fed_avg_algorithm.py:35
  *
@@ -134,6 +136,23 @@ int32_t fedavg_accumulate(fedavg_ctx* ctx, const void* const* client_ptrs, int32
 int32_t fedavg_aggregate(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
                          const double* weights, int32_t num_clients, void* const* out_ptrs,
                          int32_t out_dtype, void* stream);
+
+/*
+ * Delta updates (DeltaParameterMessage, message.py:34-61): every client tensor of the call is a
+ * delta against the server's cached global model `base_ptrs[num_segments]` (fp64 device
+ * tensors, e.g. the ModelCache copy, util/model_cache.py:27-34). The fold uses
+ * x = base + delta (fp64, rounded — exactly restore()'s `old.to(float64) + v`, message.py:54),
+ * fusing the restore into the reduce: the base is read once per tile instead of one restored
+ * fp64 copy per client. Otherwise identical to fedavg_accumulate / fedavg_aggregate (arrival
+ * order is preserved across mixed full/delta calls because the accumulator carries over).
+ */
+int32_t fedavg_accumulate_delta(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                                const double* weights, int32_t num_clients,
+                                const void* const* base_ptrs, void* stream);
+int32_t fedavg_aggregate_delta(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                               const double* weights, int32_t num_clients,
+                               const void* const* base_ptrs, void* const* out_ptrs,
+                               int32_t out_dtype, void* stream);
 
 /*
  * Non-streaming ratio path (accumulate=False): out = sum_k ratio[k] * x_k in fp64, no

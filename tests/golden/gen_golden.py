@@ -173,6 +173,15 @@ def build_cases():
         a[3]["training_loss"] = [0.5, 1.5, 2.5][i]
         a[3]["epoch"] = 3
 
+    # delta updates restored against the cached global model (message.py:40-61), mixed with a
+    # full update, exactly as AggregationServer feeds them (aggregation_server.py:121-129)
+    c = add("delta_restore", {"d0": (3001,), "d1": (17, 9)}, torch.float64, 5, [120, 4000, 33, 950, 7], 57)
+    g = torch.Generator().manual_seed(570)
+    c["old"] = {"d0": torch.randn(3001, generator=g, dtype=torch.float64),
+                "d1": torch.randn(17, 9, generator=g, dtype=torch.float64)}
+    c["kinds"] = ["delta", "delta", "full", "delta", "delta"]
+    c["arrivals"][2] = (2, {k: v.to(torch.float32) for k, v in c["arrivals"][2][1].items()}, 33, {})
+
     # ---- errors ----
     c = add("err_nan_input", {"e": (100,)}, torch.float32, 3, [1, 2, 3], 60)
     c["arrivals"][1][1]["e"][17] = float("nan")
@@ -206,13 +215,22 @@ def run_reference(case, message, fed):
         algo = FedAVG()
     algo.accumulate = case["accumulate"]
     algo.aggregate_loss = case["aggregate_loss"]
-    for wid, params, weight, other in case["arrivals"]:
+    kinds = case.get("kinds") or ["full"] * len(case["arrivals"])
+    for (wid, params, weight, other), kind in zip(case["arrivals"], kinds):
         if params is None:
             algo.process_worker_data(worker_id=wid, worker_data=None)
             continue
         od = dict(other)
-        msg = message.ParameterMessage(parameter={k: v.clone() for k, v in params.items()},
-                                       aggregation_weight=weight, other_data=od)
+        if kind == "delta":
+            # AggregationServer._process_worker_data: data = data.restore(old_parameter)
+            dmsg = message.DeltaParameterMessage(delta_parameter={k: v.clone() for k, v in params.items()},
+                                                 aggregation_weight=weight, other_data=od)
+            msg = dmsg.restore({k: v.clone() for k, v in case["old"].items()})
+        else:
+            msg = message.ParameterMessage(parameter={k: v.clone() for k, v in params.items()},
+                                           aggregation_weight=weight, other_data=od)
+            if "old" in case:
+                msg.complete(case["old"])
         algo.process_worker_data(worker_id=wid, worker_data=msg)
     return algo.aggregate_worker_data()
 
@@ -245,7 +263,12 @@ def main() -> int:
             "aggregate_loss": case["aggregate_loss"],
             "per_tensor_weight": case["per_tensor_weight"],
             "arrivals": [],
+            "kinds": case.get("kinds"),
         }
+        if "old" in case:
+            entry["old_keys"] = list(case["old"].keys())
+            for k, v in case["old"].items():
+                arrays[f"{name}/old/{k}"] = _np(v)
         for j, (wid, params, weight, other) in enumerate(case["arrivals"]):
             a = {"worker_id": wid, "weight": weight, "other_data": other,
                  "keys": None if params is None else list(params.keys())}

@@ -34,6 +34,8 @@ class GoldenCase:
     error: str | None
     expected: dict[str, np.ndarray] | None
     meta: dict
+    kinds: list[str] | None = None  # per arrival "full" / "delta" (delta: against `old`)
+    old: dict[str, np.ndarray] | None = None
 
     def torch_params(self, arrival: Arrival, device: torch.device | str = "cpu") -> dict[str, torch.Tensor]:
         assert arrival.arrays is not None
@@ -74,6 +76,8 @@ def load_golden() -> dict[str, GoldenCase]:
             error=c["error"],
             expected=expected,
             meta=c,
+            kinds=c.get("kinds"),
+            old={k: data[f"{name}/old/{k}"] for k in c["old_keys"]} if c.get("old_keys") else None,
         )
     return cases
 

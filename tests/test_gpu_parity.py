@@ -18,6 +18,7 @@ import pytest
 import torch
 
 from distributed_learning_simulation_lib_amd import (
+    DeltaParameterMessage,
     FedAVGAlgorithm,
     NaNAggregationError,
     ParameterMessage,
@@ -43,12 +44,23 @@ def run_hip(case, device, wave_size, from_host=False, split_policy=1):
         algo = FedAVGAlgorithm(device=device, wave_size=wave_size, split_policy=split_policy)
     algo.accumulate = case.accumulate
     algo.aggregate_loss = case.aggregate_loss
-    for a in case.arrivals:
+    kinds = case.kinds or ["full"] * len(case.arrivals)
+    old = None
+    if case.old is not None:
+        old = {k: torch.from_numpy(v.copy()) for k, v in case.old.items()}  # the server's fp64 host cache
+        algo.set_old_parameter(old)
+    for a, kind in zip(case.arrivals, kinds):
         if a.arrays is None:
             algo.process_worker_data(a.worker_id, None)
             continue
         params = case.torch_params(a, "cpu" if from_host else device)
-        msg = ParameterMessage(parameter=params, aggregation_weight=a.weight, other_data=dict(a.other_data))
+        if kind == "delta":
+            msg = DeltaParameterMessage(delta_parameter=params, aggregation_weight=a.weight,
+                                        other_data=dict(a.other_data))
+        else:
+            msg = ParameterMessage(parameter=params, aggregation_weight=a.weight, other_data=dict(a.other_data))
+            if old is not None:
+                msg.complete(old)
         algo.process_worker_data(a.worker_id, msg)
     try:
         return algo.aggregate_worker_data()

@@ -69,3 +69,28 @@ def test_config1_loopback_hip(hip_device):
         assert got.dtype == np.float64
         assert np.array_equal(got.view(np.uint64), expected(r, srv.arrivals[r]).view(np.uint64))
     print(f"config 1 loopback (HIP): {ROUNDS} rounds in {elapsed:.2f} s, per round {srv.round_seconds}")
+
+
+@pytest.mark.gpu
+def test_server_delta_rounds_hip_vs_oracle(hip_device):
+    """Round 1 full updates, round 2 delta updates: the HIP algorithm gets the deltas unrestored
+    (fused restore, fedavg_*_delta); the oracle server restores on the host. Bit-identical."""
+    from distributed_learning_simulation_lib_amd import DeltaParameterMessage, FedAVGAlgorithm
+    from distributed_learning_simulation_lib_amd.message import ParameterMessage
+
+    def rounds(srv):
+        g = torch.Generator().manual_seed(3)
+        shapes = {"w": (4099,), "b": (33,)}
+        for wid in range(3):
+            srv._process_worker_data(wid, ParameterMessage(
+                parameter={k: torch.randn(s, generator=g) for k, s in shapes.items()}, aggregation_weight=10 + wid))
+        for wid in range(3):
+            delta = {k: torch.randn(s, generator=g, dtype=torch.float64) * 1e-3 for k, s in shapes.items()}
+            srv._process_worker_data(wid, DeltaParameterMessage(delta_parameter=delta, aggregation_weight=7 * wid + 1))
+        return srv.results
+
+    hip = rounds(AggregationServer(algorithm=FedAVGAlgorithm(device=hip_device), worker_number=3, round_number=2))
+    ref = rounds(AggregationServer(algorithm=OracleAlgorithm(), worker_number=3, round_number=2))
+    for rh, rr in zip(hip, ref):
+        for k in rr.parameter:
+            assert torch.equal(rh.parameter[k].view(torch.int64), rr.parameter[k].view(torch.int64)), k

@@ -2,7 +2,7 @@
 
 import pytest
 
-from oracle.fedavg_oracle import OracleFedAvg, OracleMessage
+from oracle.fedavg_oracle import OracleFedAvg, OracleMessage, complete, restore
 from tests.golden_io import bits_equal, load_golden
 
 CASES = load_golden()
@@ -15,11 +15,17 @@ def run_oracle(case):
         def get_weight(m, name):
             return ptw[name][int(m.aggregation_weight)]
     algo = OracleFedAvg(accumulate=case.accumulate, aggregate_loss=case.aggregate_loss, get_weight=get_weight)
-    for a in case.arrivals:
+    kinds = case.kinds or ["full"] * len(case.arrivals)
+    for a, kind in zip(case.arrivals, kinds):
         if a.arrays is None:
             algo.process_worker_data(a.worker_id, None)
             continue
-        msg = OracleMessage(parameter=dict(a.arrays), aggregation_weight=a.weight,
+        params = dict(a.arrays)
+        if kind == "delta":
+            params = restore(params, case.old)
+        elif case.old is not None:
+            complete(params, case.old)
+        msg = OracleMessage(parameter=params, aggregation_weight=a.weight,
                             other_data=dict(a.other_data), dtype=case.dtype)
         algo.process_worker_data(a.worker_id, msg)
     return algo.aggregate_worker_data()

@@ -229,7 +229,7 @@ def main() -> int:
     ap.add_argument("--layout", default="resnet18", choices=sorted(LAYOUTS))
     ap.add_argument("--clients-per-gpu", type=int, default=64)
     ap.add_argument("--wave", type=int, default=0, help="clients per launch (streaming waves); 0 = all")
-    ap.add_argument("--chunks", type=int, default=8)
+    ap.add_argument("--chunks", type=int, default=2)
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -79,6 +79,12 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
         [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_int32, POINTER(c_void_p)],
     ),
     "fedavg_plan_run": (c_int32, [c_void_p, c_void_p]),
+    "fedavg_plan_create_partial": (
+        c_int32,
+        [c_void_p, _PP, c_int32, _PD, c_int32, c_int32, POINTER(c_void_p)],
+    ),
+    "fedavg_plan_create_finalize": (c_int32, [c_void_p, _PD, _PP, c_int32, POINTER(c_void_p)]),
+    "fedavg_plan_run_range": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_plan_destroy": (c_int32, [c_void_p]),
     "fedavg_check": (c_int32, [c_void_p, c_void_p, POINTER(c_uint32)]),
     "fedavg_find_nan_clients": (

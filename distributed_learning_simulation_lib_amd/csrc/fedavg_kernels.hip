@@ -75,7 +75,7 @@ constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
 // efficiency; nt stores cut that), AE 16 / CU 512 B +-1 %, load fence / 128-512-thread
 // groups / fused fold within noise. Shipped: AE 8, CU 256 B, nt loads and stores.
 #ifndef FEDAVG_AE
-#define FEDAVG_AE 8
+#define FEDAVG_AE 16
 #endif
 #ifndef FEDAVG_CU_BYTES
 #define FEDAVG_CU_BYTES 256
@@ -88,6 +88,9 @@ constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
 #endif
 #ifndef FEDAVG_MIN_WAVES  // __launch_bounds__ minimum waves per SIMD (caps VGPRs: 8 -> <= 64)
 #define FEDAVG_MIN_WAVES 1
+#endif
+#ifndef FEDAVG_PERSISTENT  // exact-order kernel as a persistent grid (resident blocks x CUs)
+#define FEDAVG_PERSISTENT 0
 #endif
 #ifndef FEDAVG_ABLATE_EPILOGUE
 #define FEDAVG_ABLATE_EPILOGUE 0
@@ -129,6 +132,7 @@ struct KArgs {
   double* acc;
   uint32_t* flag;
   int32_t tile_begin;
+  int32_t num_tiles;   // tiles of this launch (persistent grid-stride bound)
   int32_t K;           // row stride of the [T][K] tables
   int32_t zero_init;   // start every segment at the identity -0.0, ignore acc_in (shard partials)
 };
@@ -625,12 +629,20 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 template <typename T, int OUT, int SPLIT, bool VEC, int FOLD>
 __global__ __launch_bounds__((SPLIT == 1) ? kThreads1 : kThreads, FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
-  const TileDesc td = load_tile(a.tiles, a.tile_begin + blockIdx.x);
   constexpr int TILE = ((SPLIT == 1) ? kThreads1 : kThreads / SPLIT) * kAE;
-  if (td.count == TILE) {
-    tile_body<T, OUT, SPLIT, VEC, true, FOLD>(a, td, lds);
-  } else {
-    tile_body<T, OUT, SPLIT, VEC, false, FOLD>(a, td, lds);
+  // Persistent form (exact-order kernel): a grid of (resident blocks) workgroups walks the
+  // tiles with stride gridDim.x, so the tiles in flight at any moment are one contiguous range
+  // of every client bucket and no block is launched per tile. The split kernel keeps one
+  // tile per workgroup (its LDS combine ends with the non-zero waves leaving).
+  const int ntiles = (SPLIT == 1) ? a.num_tiles : static_cast<int>(gridDim.x);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const TileDesc td = load_tile(a.tiles, a.tile_begin + t);
+    if (td.count == TILE) {
+      tile_body<T, OUT, SPLIT, VEC, true, FOLD>(a, td, lds);
+    } else {
+      tile_body<T, OUT, SPLIT, VEC, false, FOLD>(a, td, lds);
+    }
+    if constexpr (SPLIT > 1) break;
   }
 }
 
@@ -735,6 +747,7 @@ struct fedavg_ctx {
 
   int split_policy = 1;  // 1 exact client order (default), 0 auto, 2 always split
   bool allow_fma = true;  // fused fold when every product is provably exact
+  int persistent_blocks = 0;  // grid cap of the exact-order kernel (0 = one block per tile)
   // profiling
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -794,12 +807,15 @@ struct Staged {
 }  // namespace
 
 struct fedavg_plan {
+  enum Kind { AGGREGATE = 0, PARTIAL = 1, FINALIZE = 2 };
   fedavg_ctx* ctx = nullptr;
   Staged st;
   char* dev = nullptr;
   int32_t in_dtype = 0;
   int out_kind = 0;
   int split = 1;
+  int kind = AGGREGATE;
+  int32_t zero_init = 0;
 };
 
 namespace {
@@ -1016,8 +1032,11 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     te = te_split1;
   }
   a.tile_begin = tb;
-  const int nblocks = te - tb;
-  if (nblocks <= 0) return FEDAVG_OK;
+  a.num_tiles = te - tb;
+  if (a.num_tiles <= 0) return FEDAVG_OK;
+  // exact-order kernel: persistent grid of at most (resident blocks) workgroups
+  const int nblocks = (split == 1 && c->persistent_blocks > 0) ? std::min(a.num_tiles, c->persistent_blocks)
+                                                               : a.num_tiles;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof) {
     e0 = take_event(c);
@@ -1111,6 +1130,19 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   c->valid.assign(num_segments, 0);
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);
+#if FEDAVG_PERSISTENT
+  {
+    int per_cu = 0, cus = 0;
+    hipDeviceProp_t prop;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA>),
+            kThreads1, 0) == hipSuccess &&
+        hipGetDeviceProperties(&prop, device) == hipSuccess) {
+      cus = prop.multiProcessorCount;
+      c->persistent_blocks = std::max(1, per_cu) * cus;
+    }
+  }
+#endif
   if (c->tiles1.size() > static_cast<size_t>(INT32_MAX / 2)) {
     delete c;
     return fail(FEDAVG_ERR_INVALID, "layout too large");
@@ -1552,8 +1584,87 @@ int32_t fedavg_plan_create(fedavg_ctx* c, const void* const* client_ptrs, int32_
   return FEDAVG_OK;
 }
 
+namespace {
+// Stage a plan's blob once into its own device buffer.
+int32_t upload_plan(fedavg_plan* p, std::vector<char>& blob, const BlobLayout& L) {
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->dev), L.bytes);
+  if (e == hipSuccess) e = hipMemcpy(p->dev, blob.data(), L.bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("plan upload: ") + hipGetErrorString(e));
+  L.point(p->dev, p->st.tab);
+  return FEDAVG_OK;
+}
+}  // namespace
+
+int32_t fedavg_plan_create_partial(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                                   const double* weights, int32_t K, int32_t zero_init, fedavg_plan** out) {
+  FEDAVG_RET(check_ctx(c));
+  if (!out) return fail(FEDAVG_ERR_INVALID, "null out");
+  *out = nullptr;
+  FEDAVG_RET(check_clients(c, client_ptrs, weights, K, in_dtype));
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  auto* p = new fedavg_plan();
+  p->ctx = c;
+  p->kind = fedavg_plan::PARTIAL;
+  p->in_dtype = K > 0 ? in_dtype : FEDAVG_F32;
+  p->out_kind = OUT_ACC;
+  p->zero_init = zero_init ? 1 : 0;
+  const BlobLayout L(c->T, std::max(K, 1));
+  std::vector<int32_t> acc_in(c->T, zero_init ? 0 : 1);  // a continuing partial reads every segment
+  std::vector<char> blob;
+  build_blob(c, K > 0 ? client_ptrs : nullptr, weights, K, nullptr, nullptr, acc_in.data(), p->st, blob, L);
+  const int32_t r = upload_plan(p, blob, L);
+  if (r != FEDAVG_OK) {
+    delete p;
+    return r;
+  }
+  p->split = 1;  // tile ranges are defined on the exact-order tiles
+  *out = p;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_plan_create_finalize(fedavg_ctx* c, const double* total_weights, void* const* out_ptrs,
+                                    int32_t out_dtype, fedavg_plan** out) {
+  FEDAVG_RET(check_ctx(c));
+  if (!out) return fail(FEDAVG_ERR_INVALID, "null out");
+  *out = nullptr;
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (!out_ptrs || !total_weights) return fail(FEDAVG_ERR_INVALID, "null output table or total weights");
+  for (int t = 0; t < c->T; ++t)
+    if (!out_ptrs[t]) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  auto* p = new fedavg_plan();
+  p->ctx = c;
+  p->kind = fedavg_plan::FINALIZE;
+  p->in_dtype = FEDAVG_F32;
+  p->out_kind = ok;
+  const BlobLayout L(c->T, 1);
+  std::vector<int32_t> acc_in(c->T, 1);
+  std::vector<char> blob;
+  build_blob(c, nullptr, nullptr, 0, out_ptrs, total_weights, acc_in.data(), p->st, blob, L);
+  const int32_t r = upload_plan(p, blob, L);
+  if (r != FEDAVG_OK) {
+    delete p;
+    return r;
+  }
+  *out = p;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_plan_run_range(fedavg_plan* p, int32_t tb, int32_t te, void* stream) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind == fedavg_plan::AGGREGATE) return fail(FEDAVG_ERR_INVALID, "aggregate plans run whole (fedavg_plan_run)");
+  fedavg_ctx* c = p->ctx;
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (te < 0) te = n;
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, p->zero_init, tb, te);
+}
+
 int32_t fedavg_plan_run(fedavg_plan* p, void* stream) {
   if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind != fedavg_plan::AGGREGATE) return fedavg_plan_run_range(p, 0, -1, stream);
   fedavg_ctx* c = p->ctx;
   for (int t = 0; t < c->T; ++t)
     if (c->valid[t]) return fail(FEDAVG_ERR_STATE, "plan run on a context holding accumulated data");

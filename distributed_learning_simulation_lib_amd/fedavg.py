@@ -391,6 +391,32 @@ class FedAvgContext:
         )
         return AggregatePlan(self, h, keep=(table, outs))
 
+    def plan_partial(self, table: ClientTable | None, in_dtype: torch.dtype, zero_init: bool = True) -> AggregatePlan:
+        """Prepared shard partial; ``plan.run_range(tb, te)`` == ``partial(table, ..., tb, te)``."""
+        n = 0 if table is None else table.num_clients
+        if table is not None:
+            self._check_table(table, in_dtype)
+            p, w = table.arrays()
+        else:
+            p, w = np.zeros(1, np.uint64), np.zeros(1, np.float64)
+        h = ctypes.c_void_p()
+        _native.check(
+            self._lib.fedavg_plan_create_partial(
+                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype) if n else _native.F32,
+                w.ctypes.data_as(_DBL), n, 1 if zero_init else 0, ctypes.byref(h),
+            )
+        )
+        return AggregatePlan(self, h, keep=(table,))
+
+    def plan_finalize(self, total_weights: Sequence[float], outs: Sequence[torch.Tensor] | OutputTable,
+                      out_dtype: torch.dtype) -> AggregatePlan:
+        """Prepared finalize with baked totals; ``plan.run_range(tb, te)`` == ``finalize_range``."""
+        ot = self._out_table(outs, out_dtype)
+        tw = (ctypes.c_double * self.layout.num_segments)(*[float(x) for x in total_weights])
+        h = ctypes.c_void_p()
+        _native.check(self._lib.fedavg_plan_create_finalize(self._h, tw, ot, out_code(out_dtype), ctypes.byref(h)))
+        return AggregatePlan(self, h, keep=(outs,))
+
     def set_fused_fold(self, enable: bool) -> None:
         """Allow the one-instruction fold when every product is provably exact (default on)."""
         _native.check(self._lib.fedavg_set_fused_fold(self._h, 1 if enable else 0))
@@ -457,6 +483,9 @@ class AggregatePlan:
 
     def run(self) -> None:
         _native.check(self.ctx._lib.fedavg_plan_run(self._h, self.ctx.stream))
+
+    def run_range(self, tile_begin: int, tile_end: int) -> None:
+        _native.check(self.ctx._lib.fedavg_plan_run_range(self._h, tile_begin, tile_end, self.ctx.stream))
 
     def close(self) -> None:
         if self._h is not None and self._h.value:

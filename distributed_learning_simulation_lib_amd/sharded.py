@@ -79,6 +79,10 @@ class HipLocalReducer:
         self.out_dtype = out_dtype
         self.prior_waves = list(prior_waves)
         self.accumulator = ctx.accumulator
+        self._partial_plan = None
+        self._finalize_plan = None
+        self._finalize_totals: list[float] | None = None
+        self.comm_stream = torch.cuda.Stream(ctx.device) if ctx.accumulator.is_cuda else None
 
     @property
     def num_tiles(self) -> int:
@@ -94,15 +98,33 @@ class HipLocalReducer:
             self.ctx.accumulate(t, self.in_dtype)
 
     def partial(self, tile_begin: int, tile_end: int) -> None:
-        self.ctx.partial(self.table, self.in_dtype, zero_init=not self.prior_waves,
-                         tile_begin=tile_begin, tile_end=tile_end)
+        # prepared once: each chunk is a bare launch (the host must stay ahead of 8 chunk
+        # kernels of ~65 us each, or the GPU idles between them)
+        if self.use_plan:
+            if self._partial_plan is None:
+                self._partial_plan = self.ctx.plan_partial(self.table, self.in_dtype, zero_init=not self.prior_waves)
+            self._partial_plan.run_range(tile_begin, tile_end)
+        else:
+            self.ctx.partial(self.table, self.in_dtype, zero_init=not self.prior_waves,
+                             tile_begin=tile_begin, tile_end=tile_end)
 
     def set_accumulated(self, total_weights: Sequence[float]) -> None:
-        self.ctx.set_accumulated(total_weights)
+        totals = [float(w) for w in total_weights]
+        if self.use_plan:
+            if self._finalize_plan is None or self._finalize_totals != totals:
+                assert self.outs is not None
+                self._finalize_plan = self.ctx.plan_finalize(totals, self.outs, self.out_dtype)
+                self._finalize_totals = totals
+        else:
+            self.ctx.set_accumulated(totals)
 
     def finalize_range(self, tile_begin: int, tile_end: int) -> None:
         assert self.outs is not None
-        self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
+        if self.use_plan:
+            assert self._finalize_plan is not None
+            self._finalize_plan.run_range(tile_begin, tile_end)
+        else:
+            self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
 
     def fused(self) -> None:
         """Single-rank shortcut: fold + divide in the last wave's launch, no extra fp64 pass."""
@@ -154,13 +176,30 @@ def sharded_reduce(
     global_totals = [float(w) for w in global_total_weights]
     reducer.prefold()
     bounds = chunk_bounds(reducer.num_tiles, chunks)
+    acc = reducer.accumulator
     works = []
-    for tb, te in bounds:
-        reducer.partial(tb, te)
-        a, b = reducer.tile_range(tb, te)
-        works.append(
-            dist.reduce(reducer.accumulator[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True)
-        )
+    comm = getattr(reducer, "comm_stream", None)
+    if acc.is_cuda and comm is not None:
+        # 1) every chunk's partial kernel goes into the compute stream back to back, each
+        #    followed by an event; 2) the reduces are issued from a side stream that waits only
+        #    for its own chunk's event, so the reduce of chunk c runs under the partial of c+1
+        compute = torch.cuda.current_stream(acc.device)
+        events = []
+        for tb, te in bounds:
+            reducer.partial(tb, te)
+            ev = torch.cuda.Event()
+            ev.record(compute)
+            events.append(ev)
+        with torch.cuda.stream(comm):
+            for (tb, te), ev in zip(bounds, events):
+                comm.wait_event(ev)
+                a, b = reducer.tile_range(tb, te)
+                works.append(dist.reduce(acc[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    else:
+        for tb, te in bounds:
+            reducer.partial(tb, te)
+            a, b = reducer.tile_range(tb, te)
+            works.append(dist.reduce(acc[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True))
     if rank == root:
         reducer.set_accumulated(global_totals)
     for (tb, te), w in zip(bounds, works):

@@ -202,6 +202,15 @@ int32_t fedavg_plan_create(fedavg_ctx* ctx, const void* const* client_ptrs, int3
                            int32_t out_dtype, fedavg_plan** out);
 int32_t fedavg_plan_run(fedavg_plan* plan, void* stream);
 int32_t fedavg_plan_destroy(fedavg_plan* plan);
+/* Plans for the multi-GPU shard step, launched per tile range (chunked collective):
+ * a partial plan is fedavg_partial(ctx, <clients>, zero_init, tb, te); a finalize plan is
+ * fedavg_finalize_range with the given per-segment total weights baked in. */
+int32_t fedavg_plan_create_partial(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                                   const double* weights, int32_t num_clients, int32_t zero_init,
+                                   fedavg_plan** out);
+int32_t fedavg_plan_create_finalize(fedavg_ctx* ctx, const double* total_weights,
+                                    void* const* out_ptrs, int32_t out_dtype, fedavg_plan** out);
+int32_t fedavg_plan_run_range(fedavg_plan* plan, int32_t tile_begin, int32_t tile_end, void* stream);
 
 /*
  * Synchronise `stream` and report the NaN flag: FEDAVG_OK, FEDAVG_ERR_NAN_ACCUM or

@@ -13,10 +13,11 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "w8": {"FEDAVG_MIN_WAVES": 8},
-    "w6": {"FEDAVG_MIN_WAVES": 6},
-    "w8_cu128": {"FEDAVG_MIN_WAVES": 8, "FEDAVG_CU_BYTES": 128},
-    "w4_ae16": {"FEDAVG_MIN_WAVES": 4, "FEDAVG_AE": 16},
+    "ae8": {"FEDAVG_AE": 8},
+    "cu128": {"FEDAVG_CU_BYTES": 128},
+    "cu512": {"FEDAVG_CU_BYTES": 512},
+    "t128": {"FEDAVG_THREADS1": 128},
+    "ae32_cu512": {"FEDAVG_AE": 32, "FEDAVG_CU_BYTES": 512},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

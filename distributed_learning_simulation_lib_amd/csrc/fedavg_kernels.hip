@@ -58,11 +58,7 @@ int32_t fail(int32_t code, const std::string& msg) {
 // ---------------------------------------------------------------------------------------
 // device-side descriptors
 // ---------------------------------------------------------------------------------------
-#ifndef FEDAVG_THREADS1
-#define FEDAVG_THREADS1 256
-#endif
 constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
-constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
 // Tuning knobs (compile-time; the shipped values were picked on MI355X by
 // scripts/tune_kernel.py, see DESIGN.md "Kernel tuning"):
 //   FEDAVG_AE        elements owned by one lane (= fp64 accumulators per lane)
@@ -76,6 +72,12 @@ constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
 // groups / fused fold within noise. Shipped: AE 8, CU 256 B, nt loads and stores.
 #ifndef FEDAVG_AE
 #define FEDAVG_AE 16
+#endif
+#ifndef FEDAVG_AE_HALF  // elements per lane for 2-byte inputs (fp16 / bf16)
+#define FEDAVG_AE_HALF 8
+#endif
+#ifndef FEDAVG_TILE1  // elements per tile of the exact-order kernel (all dtypes)
+#define FEDAVG_TILE1 4096
 #endif
 #ifndef FEDAVG_CU_BYTES
 #define FEDAVG_CU_BYTES 256
@@ -99,8 +101,8 @@ constexpr int kThreads1 = FEDAVG_THREADS1;  // exact-order kernel workgroup size
 #define FEDAVG_NT_STORE 1
 #endif
 constexpr int kAE = FEDAVG_AE;    // elements owned by one lane (fp64 accumulators per lane)
-constexpr int kTile1 = kThreads1 * kAE;       // 2048 elements, SPLIT = 1
-constexpr int kTile4 = (kThreads / 4) * kAE;  // 512 elements,  SPLIT = 4
+constexpr int kTile1 = FEDAVG_TILE1;          // 4096 elements, SPLIT = 1 (any dtype)
+constexpr int kTile4 = (kThreads / 4) * kAE;  // 1024 elements, SPLIT = 4
 
 struct TileDesc {
   int32_t seg;
@@ -280,11 +282,11 @@ __device__ __forceinline__ double load_g<bf16_t>(gptr<const bf16_t> p, int64_t i
 // Loads of one client's share of a tile for one lane: VPL vectors of 16 B, expanded to
 // kAE doubles. Element index (within the tile) of vector v of lane li: (v*LANES + li)*N,
 // so one wave-instruction reads 1 KiB contiguous.
-template <typename T, int LANES, bool FULL, bool VEC>
+template <typename T, int LANES, bool FULL, bool VEC, int AE>
 struct LaneLoader {
   using V = typename Vec16<T>::type;
   static constexpr int N = Vec16<T>::n;
-  static constexpr int VPL = kAE / N;
+  static constexpr int VPL = AE / N;
 
   // raw 16-B loads (fast path: whole tile, aligned buffers)
   __device__ __forceinline__ static void load_raw(gptr<const T> base, int li, V (&buf)[VPL]) {
@@ -301,7 +303,7 @@ struct LaneLoader {
 
   // bounds-checked loads straight to doubles (segment tails, unaligned buffers)
   __device__ __forceinline__ static void load_checked(gptr<const T> base, int li, int count,
-                                                      double (&x)[kAE]) {
+                                                      double (&x)[AE]) {
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int e = (v * LANES + li) * N;
@@ -317,6 +319,22 @@ struct LaneLoader {
 };
 
 // One tile of the weighted reduce. See the file header for the algorithm.
+// Launch geometry. The exact-order kernel (SPLIT = 1) tiles every dtype the same way
+// (kTile1 elements, so one tile table serves all calls) but gives each lane a dtype-dependent
+// slice: 16 elements (fp32 / fp64: a client's tile slice is 16 KiB resp. 32 KiB contiguous,
+// 4 / 2 clients in flight per group) or 8 (fp16 / bf16: 512-lane workgroups, 16 clients per
+// group) — the fastest shapes measured on MI355X. The split kernel keeps kAE for all dtypes.
+template <typename T, int SPLIT>
+struct Geo {
+  static constexpr int AE = (SPLIT > 1) ? kAE : (sizeof(T) == 2 ? FEDAVG_AE_HALF : kAE);
+  static constexpr int LANES = (SPLIT > 1) ? 64 : kTile1 / AE;
+  static constexpr int THREADS = (SPLIT > 1) ? kThreads : LANES;
+  static constexpr int TILE = LANES * AE;
+  static_assert(SPLIT == 1 || TILE == kTile4, "split tiles");
+  static_assert(SPLIT > 1 || TILE == kTile1, "tile geometry");
+  static_assert(THREADS % 64 == 0 && THREADS <= 1024, "workgroup size");
+};
+
 // NaN flags live in host-coherent pinned memory, one word per condition (0: accumulator NaN,
 // 1: result NaN). A wave that sees a NaN stores 1 with system scope — no atomics, every
 // writer writes the same value — and the host reads the words after the stream drains.
@@ -361,8 +379,9 @@ __device__ __forceinline__ double fold(double acc, double x, double w, double ba
 
 template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD>
 __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
-  constexpr int LANES = (SPLIT == 1) ? kThreads1 : kThreads / SPLIT;  // lanes sharing one client stream
-  using LL = LaneLoader<T, LANES, FULL && VEC, VEC>;
+  constexpr int AE = Geo<T, SPLIT>::AE;
+  constexpr int LANES = Geo<T, SPLIT>::LANES;  // lanes sharing one client stream
+  using LL = LaneLoader<T, LANES, FULL && VEC, VEC, AE>;
   using V = typename LL::V;
   constexpr int N = LL::N;
   constexpr int VPL = LL::VPL;
@@ -394,9 +413,9 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   // for every p (including -0.0 and +0.0), and fma(x, w, -0.0) == round(x * w). Folding the
   // first client into it therefore equals the reference's assignment `acc = tmp`
   // (fed_avg_algorithm.py:55-56) bit for bit, signed zeros included, with no special case.
-  double acc[kAE];
+  double acc[AE];
 #pragma unroll
-  for (int i = 0; i < kAE; ++i) acc[i] = -0.0;
+  for (int i = 0; i < AE; ++i) acc[i] = -0.0;
   bool have = a.zero_init != 0;  // wave-uniform: "this wave holds a value for the tile"
   if ((SPLIT == 1 || wave == 0) && !a.zero_init && to_const<int32_t>(a.tab.acc_in)[seg]) {
     const gptr<const double> ap = to_global<double>(a.acc + acc_base);
@@ -420,9 +439,9 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 
   // delta calls: the base model's slice of this tile, fp64, read once per tile (L2-shared
   // by nothing else: one read of the base per fold, like one more client)
-  double base[kAE];
+  double base[AE];
 #pragma unroll
-  for (int i = 0; i < kAE; ++i) base[i] = 0.0;
+  for (int i = 0; i < AE; ++i) base[i] = 0.0;
   if constexpr (FOLD == FOLD_DELTA) {
     const gptr<const double> bp =
         to_global<double>(reinterpret_cast<const void*>(to_const<uint64_t>(a.tab.base)[seg])) + td.start;
@@ -486,21 +505,21 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   } else {
     for (int k = kb; k < ke; ++k) {
       const double wk = wp[k];
-      double x[kAE];
+      double x[AE];
       LL::load_checked(client(k), li, count, x);
 #pragma unroll
-      for (int i = 0; i < kAE; ++i) acc[i] = fold<FOLD>(acc[i], x[i], wk, base[i]);
+      for (int i = 0; i < AE; ++i) acc[i] = fold<FOLD>(acc[i], x[i], wk, base[i]);
     }
   }
   have = have || (ke > kb);
 
   if constexpr (SPLIT > 1) {
     // stage wave partials in LDS; wave 0 folds them in wave order
-    int* have_lds = reinterpret_cast<int*>(lds + (SPLIT - 1) * 64 * kAE);
+    int* have_lds = reinterpret_cast<int*>(lds + (SPLIT - 1) * 64 * AE);
     if (wave > 0) {
-      double* dst = lds + ((wave - 1) * 64 + li) * kAE;
+      double* dst = lds + ((wave - 1) * 64 + li) * AE;
 #pragma unroll
-      for (int i = 0; i < kAE; ++i) dst[i] = acc[i];
+      for (int i = 0; i < AE; ++i) dst[i] = acc[i];
       if (li == 0) have_lds[wave - 1] = have ? 1 : 0;
     }
     __syncthreads();
@@ -508,13 +527,13 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
     for (int w2 = 1; w2 < SPLIT; ++w2) {
       if (have_lds[w2 - 1]) {
-        const double* src = lds + ((w2 - 1) * 64 + li) * kAE;
+        const double* src = lds + ((w2 - 1) * 64 + li) * AE;
         if (have) {
 #pragma unroll
-          for (int i = 0; i < kAE; ++i) acc[i] = acc[i] + src[i];
+          for (int i = 0; i < AE; ++i) acc[i] = acc[i] + src[i];
         } else {
 #pragma unroll
-          for (int i = 0; i < kAE; ++i) acc[i] = src[i];
+          for (int i = 0; i < AE; ++i) acc[i] = src[i];
         }
         have = true;
       }
@@ -554,9 +573,9 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     // fused divide (_apply_total_weight, :71-74) + NaN check of the result (:97)
     const double W = to_const<double>(a.tab.wtot)[seg];
     bool bad_res = false;
-    double res[kAE];
+    double res[AE];
 #pragma unroll
-    for (int i = 0; i < kAE; ++i) {
+    for (int i = 0; i < AE; ++i) {
 #if FEDAVG_ABLATE_EPILOGUE  // timing-only build: reciprocal multiply, no NaN checks (wrong results)
       res[i] = acc[i] * (1.0 / W);
 #else
@@ -627,9 +646,9 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 }
 
 template <typename T, int OUT, int SPLIT, bool VEC, int FOLD>
-__global__ __launch_bounds__((SPLIT == 1) ? kThreads1 : kThreads, FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
+__global__ __launch_bounds__((Geo<T, SPLIT>::THREADS), FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
-  constexpr int TILE = ((SPLIT == 1) ? kThreads1 : kThreads / SPLIT) * kAE;
+  constexpr int TILE = Geo<T, SPLIT>::TILE;
   // Persistent form (exact-order kernel): a grid of (resident blocks) workgroups walks the
   // tiles with stride gridDim.x, so the tiles in flight at any moment are one contiguous range
   // of every client bucket and no block is launched per tile. The split kernel keeps one
@@ -966,7 +985,7 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
 
 template <typename T, int OUT, int SPLIT, bool VEC>
 hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s) {
-  const int threads = (SPLIT == 1) ? kThreads1 : kThreads;
+  const int threads = Geo<T, SPLIT>::THREADS;
   if (fold == FOLD_FMA) {
     hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA>), dim3(nblocks), dim3(threads), 0, s, a);
   } else if (fold == FOLD_DELTA) {
@@ -1136,7 +1155,7 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
     hipDeviceProp_t prop;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA>),
-            kThreads1, 0) == hipSuccess &&
+            Geo<float, 1>::THREADS, 0) == hipSuccess &&
         hipGetDeviceProperties(&prop, device) == hipSuccess) {
       cus = prop.multiProcessorCount;
       c->persistent_blocks = std::max(1, per_cu) * cus;

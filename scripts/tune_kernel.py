@@ -13,11 +13,9 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "ae8": {"FEDAVG_AE": 8},
-    "cu128": {"FEDAVG_CU_BYTES": 128},
-    "cu512": {"FEDAVG_CU_BYTES": 512},
-    "t128": {"FEDAVG_THREADS1": 128},
-    "ae32_cu512": {"FEDAVG_AE": 32, "FEDAVG_CU_BYTES": 512},
+    "h16": {"FEDAVG_AE_HALF": 16},
+    "h16_cu512": {"FEDAVG_AE_HALF": 16, "FEDAVG_CU_BYTES": 512},
+    "h8_cu128": {"FEDAVG_CU_BYTES": 128},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 
@@ -42,7 +40,8 @@ def run_all(rounds=7, iters=10):
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     if len(sys.argv) > 3 and sys.argv[3] == "flat":
         layout = ModelLayout.flat(layout.total_numel)
-    buckets, views = make_clients(layout, 0, K, dev, torch.float32)
+    dt = getattr(torch, sys.argv[4]) if len(sys.argv) > 4 else torch.float32
+    buckets, views = make_clients(layout, 0, K, dev, dt)
     w = dataset_size_weights(K)
     table = ClientTable(layout.num_segments)
     for row, wk in zip(views, w):
@@ -57,7 +56,7 @@ def run_all(rounds=7, iters=10):
         ctxs[name] = FedAvgContext(layout, dev, lib=lib)
         if name.endswith("_nofma"):
             ctxs[name].set_fused_fold(False)
-        ctxs[name].aggregate(table, torch.float32, outs, torch.float32)
+        ctxs[name].aggregate(table, dt, outs, torch.float32)
         torch.cuda.synchronize()
         if ref is None:
             ref = flat.clone()
@@ -68,11 +67,11 @@ def run_all(rounds=7, iters=10):
         for name, ctx in ctxs.items():
             ctx.prof_enable(True)
             for _ in range(iters):
-                ctx.aggregate(table, torch.float32, outs, torch.float32)
+                ctx.aggregate(table, dt, outs, torch.float32)
             ctx.prof_enable(False)
             ms, n = ctx.prof_collect()
             times[name].append(ms / n)
-    nbytes = K * layout.total_numel * 4 + layout.total_numel * 4
+    nbytes = K * layout.total_numel * buckets.element_size() + layout.total_numel * 4
     res = {}
     for name, t in times.items():
         med = float(np.median(t))

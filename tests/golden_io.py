@@ -87,3 +87,44 @@ def bits_equal(a: np.ndarray, b: np.ndarray) -> bool:
     a = np.ascontiguousarray(a, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64)
     return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+# ---- PersonalizedFedAVG fixtures (tests/golden/gen_personalized.py) ----------------------
+@dataclass
+class PersonalizedCase:
+    name: str
+    dtype: str
+    names: list[str]
+    shapes: list[tuple[int, ...]]
+    worker_weights: dict[int, dict[int, Any]]  # receiver -> {client: weight}, key order kept
+    arrivals: list[Arrival]  # Arrival.weight is unused (None)
+    error: str | None
+    expected: dict[int, dict[str, np.ndarray]] | None  # receiver -> {name: fp64}
+    central: dict[str, np.ndarray] | None
+    meta: dict
+
+    def torch_params(self, arrival: Arrival, device: torch.device | str = "cpu") -> dict[str, torch.Tensor]:
+        return GoldenCase.torch_params(self, arrival, device)  # type: ignore[arg-type]
+
+
+def load_personalized() -> dict[str, PersonalizedCase]:
+    manifest = json.loads((GOLDEN_DIR / "personalized_manifest.json").read_text())
+    data = np.load(GOLDEN_DIR / "personalized_golden.npz", allow_pickle=False)
+    cases = {}
+    for c in manifest["cases"]:
+        name = c["name"]
+        arrivals = []
+        for n, a in enumerate(c["arrivals"]):
+            arrays = None if a["keys"] is None else {k: data[f"{name}/in/{n}/{k}"] for k in a["keys"]}
+            arrivals.append(Arrival(a["worker_id"], None, dict(a["other_data"]), arrays))
+        expected = central = None
+        if c["error"] is None:
+            expected = {r["worker_id"]: {k: data[f"{name}/out/{r['worker_id']}/{k}"] for k in r["keys"]}
+                        for r in c["receivers"]}
+            central = {k: data[f"{name}/central/{k}"] for k in c["central_keys"]}
+        cases[name] = PersonalizedCase(
+            name=name, dtype=c["dtype"], names=c["names"], shapes=[tuple(s) for s in c["shapes"]],
+            worker_weights={j: {i: w for i, w in row} for j, row in c["worker_weights"]},
+            arrivals=arrivals, error=c["error"], expected=expected, central=central, meta=c,
+        )
+    return cases

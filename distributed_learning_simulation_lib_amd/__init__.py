@@ -6,7 +6,7 @@ HIP kernels behind the C ABI of ``include/fedavg_hip.h``; this package is the ho
 keeps the reference's plugin surface.
 """
 
-from .algorithm import AggregationAlgorithm, FedAVGAlgorithm
+from .algorithm import AggregationAlgorithm, FedAVGAlgorithm, PersonalizedFedAVGAlgorithm
 from .algorithm_repository import AlgorithmRepository
 from .fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError
 from .message import (
@@ -35,6 +35,7 @@ __all__ = [
     "NaNAggregationError",
     "ParameterMessage",
     "ParameterMessageBase",
+    "PersonalizedFedAVGAlgorithm",
     "get_message_size",
 ]
 

@@ -25,6 +25,7 @@ ERR_HIP = 5
 ERR_STATE = 6
 FLAG_ACC_NAN = 0x1
 FLAG_RESULT_NAN = 0x2
+FLAG_CENTRAL_NAN = 0x4
 ABI_VERSION = 1
 
 _PP = POINTER(c_void_p)
@@ -94,6 +95,19 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_prof_enable": (c_int32, [c_void_p, c_int32]),
     "fedavg_prof_collect": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
     "fedavg_bw_probe": (c_int32, [c_void_p, c_int64, c_void_p, c_int32, c_void_p]),
+    # PersonalizedFedAVG (personalized_kernels.hip)
+    "fedavg_pers_create": (c_int32, [POINTER(c_void_p), c_int32, POINTER(c_int64), c_int32]),
+    "fedavg_pers_destroy": (c_int32, [c_void_p]),
+    "fedavg_pers_set_fused_fold": (c_int32, [c_void_p, c_int32]),
+    "fedavg_pers_aggregate": (
+        c_int32,
+        [c_void_p, _PP, c_int32, c_int32, POINTER(c_int64), _PD, POINTER(c_int64), c_int32, _PP, c_int32,
+         _PP, c_int32, c_void_p],
+    ),
+    "fedavg_pers_check": (c_int32, [c_void_p, c_void_p, POINTER(c_uint32)]),
+    "fedavg_pers_prof_enable": (c_int32, [c_void_p, c_int32]),
+    "fedavg_pers_prof_collect": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
+    "fedavg_fp64_probe": (c_int32, [c_int64, c_int32, _PD, c_void_p]),
 }
 
 _lib: ctypes.CDLL | None = None

@@ -1,4 +1,5 @@
 from .aggregation_algorithm import AggregationAlgorithm
 from .fed_avg_algorithm import FedAVGAlgorithm
+from .personalized_aggregation_algorithm import PersonalizedFedAVGAlgorithm
 
-__all__ = ["AggregationAlgorithm", "FedAVGAlgorithm"]
+__all__ = ["AggregationAlgorithm", "FedAVGAlgorithm", "PersonalizedFedAVGAlgorithm"]

@@ -1,0 +1,228 @@
+"""PersonalizedFedAVG on MI355X: every receiver's FedAvg and the centralized average in one launch.
+
+Same plugin surface as the reference's ``PersonalizedFedAVGAlgorithm``
+(``simulation_lib/algorithm/personalized_aggregation_algorithm.py:9-57``):
+``set_worker_weights`` (:15-21), ``process_worker_data`` (:23-43), ``aggregate_worker_data``
+(:45-57) returning a ``MultipleWorkerMessage`` whose ``worker_data`` holds one
+``ParameterMessage`` per receiver (in ``worker_weights`` key order) and whose
+``other_data["centralized_parameter"]`` is the equal-weight average of them.
+
+The reference deep-copies every arriving update into M-1 per-receiver ``FedAVGAlgorithm``s
+and reduces each on the CPU (M² fp64 passes over the model). Here an arrival is staged once
+in HBM and, at the end of the round, one HIP launch folds all N arrivals into all M receivers
+(arrival-order fp64 chains, bit-identical to the reference) and the centralized average
+(``personalized_kernels.hip``). Observable differences (as for ``FedAVGAlgorithm``): the NaN
+assertions fire at ``aggregate_worker_data``, results are float64 tensors on the GPU (or on
+``result_device``), and a tensor name absent from the first arrival raises
+``NotImplementedError``.
+"""
+
+from __future__ import annotations
+
+from typing import Any
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..fedavg import ModelLayout, NaNAggregationError
+from ..ingest import HostIngest
+from ..message import Message, ModelParameter, MultipleWorkerMessage, ParameterMessage
+from ..personalized import PersonalizedContext
+from .aggregation_algorithm import (
+    AggregationAlgorithm,
+    context_for,
+    default_device,
+    split_empty,
+    to_device_operand,
+    unify_dtype,
+)
+
+
+class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
+    def __init__(
+        self,
+        device: torch.device | str | None = None,
+        result_dtype: torch.dtype = torch.float64,
+        result_device: torch.device | str | None = None,
+    ) -> None:
+        super().__init__()
+        self._worker_weights: dict[int, dict[int, float]] = {}
+        self._device = torch.device(device) if device is not None else None
+        self.result_dtype = result_dtype
+        self.result_device = torch.device(result_device) if result_device is not None else None
+        self.__arrivals: list[tuple[int, ParameterMessage, list[torch.Tensor | None]]] = []
+        self.__layout: ModelLayout | None = None
+        self.__ctx: PersonalizedContext | None = None
+        self.__ingest: HostIngest | None = None
+
+    @property
+    def device(self) -> torch.device:
+        if self._device is None:
+            self._device = default_device()
+        return self._device
+
+    # :15-21
+    def set_worker_weights(self, worker_weights: dict[int, dict[int, float]]) -> None:
+        assert not self._worker_weights
+        self._worker_weights = worker_weights
+
+    # :23-43 — the update is staged once in HBM instead of deep-copied per receiver
+    def process_worker_data(self, worker_id: int, worker_data: Message | None) -> bool:
+        assert self._worker_weights
+        if worker_data is None:
+            return True  # every receiver records a skipped worker (aggregation_algorithm.py:98-100)
+        if not any(j != worker_id for j in self._worker_weights):
+            return True  # nobody else receives it: the reference never touches it
+        assert isinstance(worker_data, ParameterMessage)
+        if self.__layout is None:
+            self.__layout = ModelLayout.from_parameters(worker_data.parameter)
+        unknown = [k for k in worker_data.parameter if k not in self.__layout.names]
+        if unknown:
+            raise NotImplementedError(
+                f"tensors {unknown} were not in the first update; complete() the message against the "
+                "global model first (aggregation_server.py:126-128)"
+            )
+        row: list[torch.Tensor | None] = []
+        for name, shape in zip(self.__layout.names, self.__layout.shapes):
+            t = worker_data.parameter.get(name)
+            if t is not None and tuple(t.shape) != shape:
+                raise ValueError(f"shape of {name} changed: {tuple(t.shape)} vs {shape}")
+            row.append(t)
+        self.__arrivals.append((worker_id, worker_data, self._to_device_row(row)))
+        return True
+
+    def _to_device_row(self, row: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
+        assert self.__layout is not None
+        host = [t for t in row if t is not None and t.device.type == "cpu"]
+        dtypes = {t.dtype for t in host}
+        if host and len(host) == sum(t is not None for t in row) and len(dtypes) == 1 and \
+                next(iter(dtypes)) in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
+            # one packed DMA per client through pinned memory (ingest.py)
+            if self.__ingest is None:
+                self.__ingest = HostIngest(self.device)
+            return self.__ingest.to_device(self.__layout, row, next(iter(dtypes)))
+        return [None if t is None else to_device_operand(t, self.device) for t in row]
+
+    # :45-57
+    def aggregate_worker_data(self) -> MultipleWorkerMessage:
+        receivers = list(self._worker_weights)
+        folded = {j: [n for n, (wid, _, _) in enumerate(self.__arrivals) if wid != j] for j in receivers}
+        for j in receivers:
+            # a receiver that heard from nobody: FedAVGAlgorithm._aggregate_parameter's
+            # `assert self.__parameter` (fed_avg_algorithm.py:88)
+            assert folded[j], f"receiver {j} received no update"
+        layout = self.__layout
+        assert layout is not None
+        parameters, central = self._reduce(receivers)
+        results: dict[int, ParameterMessage] = {}
+        for j in receivers:
+            # the receiver's FedAVGAlgorithm keeps _all_worker_data[worker_id] = update: a worker
+            # that reported twice keeps its first position and its last message
+            by_id: dict[int, Message] = {}
+            for n in folded[j]:
+                by_id[self.__arrivals[n][0]] = self.__arrivals[n][1]
+            msgs = list(by_id.values())
+            results[j] = ParameterMessage(
+                parameter=parameters[j],
+                end_training=msgs[0].end_training,
+                in_round=msgs[0].in_round,
+                other_data=self._check_and_reduce_other_data(msgs),
+            )
+        return MultipleWorkerMessage(worker_data=results, other_data={"centralized_parameter": central})
+
+    def _reduce(self, receivers: list[int]) -> tuple[dict[int, ModelParameter], ModelParameter]:
+        layout = self.__layout
+        assert layout is not None
+        native, keep = split_empty(layout)
+        M = len(receivers)
+        out: dict[int, ModelParameter] = {j: {} for j in receivers}
+        central: ModelParameter = {}
+        if native is not None:
+            rows = [[row[i] for i in keep] for _, _, row in self.__arrivals]
+            present = [t for r in rows for t in r if t is not None]
+            unified, dt = unify_dtype(present)
+            it = iter(unified)
+            rows = [[None if t is None else next(it) for t in r] for r in rows]
+            ids = [wid for wid, _, _ in self.__arrivals]
+            weights = np.zeros((M, len(ids)), dtype=np.float64)
+            for r, j in enumerate(receivers):
+                for n, wid in enumerate(ids):
+                    weights[r, n] = float(self._worker_weights[j].get(wid, 0))  # (:36)
+            if self.__ctx is None or self.__ctx.layout != native or self.__ctx.device != self.device:
+                if self.__ctx is not None:
+                    self.__ctx.close()
+                self.__ctx = PersonalizedContext(native, self.device)
+            res_dtype = self.result_dtype if self.result_dtype in (torch.float32, torch.float64) else torch.float64
+            bufs = [torch.empty(native.padded_offsets(8)[1], dtype=res_dtype, device=self.device) for _ in receivers]
+            offs, _ = native.padded_offsets(8)
+            outs = [[b[o : o + n] for o, n in zip(offs, native.numels)] for b in bufs]
+            cbuf = torch.empty(native.padded_offsets(8)[1], dtype=torch.float64, device=self.device)
+            couts = [cbuf[o : o + n] for o, n in zip(offs, native.numels)]
+            try:
+                self.__ctx.aggregate(rows, dt, ids, weights, receivers, outs, res_dtype, couts, torch.float64)
+            except _native.NativeError as e:
+                if e.status == _native.ERR_STATE:
+                    # every update a receiver folds lacks some tensor: the reference would leave
+                    # the key out of that receiver's model; complete() the messages instead
+                    raise NotImplementedError(str(e)) from e
+                raise
+            flags = self.__ctx.check()
+            if flags:
+                self._raise_nan(flags, rows, dt, native, outs, receivers)
+            for r, j in enumerate(receivers):
+                for s, i in enumerate(keep):
+                    out[j][layout.names[i]] = outs[r][s].view(layout.shapes[i])
+            for s, i in enumerate(keep):
+                central[layout.names[i]] = couts[s].view(layout.shapes[i])
+        for i, name in enumerate(layout.names):
+            if i not in keep:
+                for j in receivers:
+                    out[j][name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
+                central[name] = torch.empty(layout.shapes[i], dtype=torch.float64, device=self.device)
+        ordered = {j: {n: out[j][n] for n in layout.names} for j in receivers}
+        central = {n: central[n] for n in layout.names}
+        if self.result_device is not None:
+            ordered = {j: {k: v.to(self.result_device) for k, v in p.items()} for j, p in ordered.items()}
+            central = {k: v.to(self.result_device) for k, v in central.items()}
+        return ordered, central
+
+    def _raise_nan(self, flags: int, rows, dt, native: ModelLayout, outs, receivers) -> None:
+        """Map the fused flags onto the reference's assertions (error path only)."""
+        if flags & (_native.FLAG_ACC_NAN | _native.FLAG_RESULT_NAN):
+            if flags & _native.FLAG_ACC_NAN:
+                from ..fedavg import ClientTable
+
+                table = ClientTable(native.num_segments)
+                for r in rows:
+                    table.add_client(r, [1.0] * native.num_segments)
+                bad = context_for(native, self.device).find_nan_clients(table, dt)
+                if bad:
+                    ids = [self.__arrivals[n][0] for n in bad]
+                    raise NaNAggregationError("input", f"NaN in the update(s) of worker(s) {ids} "
+                                                       "(fed_avg_algorithm.py:35)", bad)
+                raise NaNAggregationError("accumulator", "NaN in a receiver's weighted sum, e.g. inf * 0 or "
+                                                         "inf - inf (fed_avg_algorithm.py:93)")
+            raise NaNAggregationError("result", "NaN in a receiver's average, e.g. 0 / 0 "
+                                                "(fed_avg_algorithm.py:97)")
+        raise NaNAggregationError("result", "NaN in the centralized average (aggregation_algorithm.py:73)")
+
+    @staticmethod
+    def _check_and_reduce_other_data(msgs: list[Message]) -> dict[str, Any]:
+        """fed_avg_algorithm.py:136-149, over the updates one receiver folded."""
+        merged: dict[str, Any] = {}
+        for msg in msgs:
+            for k, v in msg.other_data.items():
+                if k in merged and v != merged[k]:
+                    raise RuntimeError(f"different values on key {k}")
+                merged.setdefault(k, v)
+        return merged
+
+    def clear_worker_data(self) -> None:
+        super().clear_worker_data()
+        self.__arrivals = []
+
+    def exit(self) -> None:
+        if self.__ctx is not None:
+            self.__ctx.close()
+            self.__ctx = None

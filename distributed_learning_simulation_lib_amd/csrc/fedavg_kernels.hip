@@ -1082,6 +1082,12 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
 
 }  // namespace
 
+// Shared with the other translation units of the library (personalized_kernels.hip): one
+// thread-local last-error string behind fedavg_last_error().
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_fail(int32_t code, const char* msg) {
+  return fail(code, msg);
+}
+
 // =======================================================================================
 // exported C ABI (include/fedavg_hip.h)
 // =======================================================================================

@@ -1,0 +1,828 @@
+// personalized_kernels.hip — gfx950 kernel of the server-side PersonalizedFedAVG reduce.
+//
+// What the reference computes (simulation_lib/algorithm/personalized_aggregation_algorithm.py):
+//   every receiver j of worker_weights keeps its own FedAVGAlgorithm (:15-21); an arriving
+//   update of worker i is deep-copied into every receiver j != i with the weight
+//   worker_weights[j].get(i, 0) (:29-43), i.e. per receiver, per named tensor t:
+//       acc_j[t] = round(x_i.to(f64) * w_ji)  (first)  /  acc_j[t] + round(x_i * w_ji)
+//       W_j[t]  += w_ji                                   (fed_avg_algorithm.py:43-64)
+//   out_j[t] = acc_j[t] / W_j[t] with the NaN assertions (fed_avg_algorithm.py:88-97), and
+//   central[t] = sum over receivers j in key order of round(out_j[t] * (1/M))
+//   (weighted_avg, aggregation_algorithm.py:51-76, called at :51-53).
+//
+// Shape: out = W · X for an [M x N] weight matrix and N client rows — but every receiver's
+// sum must be the arrival-order fp64 chain with separately rounded products to stay
+// bit-identical, which no MFMA instruction computes (its internal reduction order and
+// rounding are not the reference's). So the contraction runs on the fp64 VALU, register-
+// blocked:
+//   * a workgroup owns a 128-element chunk of one segment (64 lanes x 2 elements) and up to
+//     64 receivers: wave w holds the fp64 accumulators of receivers [16w, 16w+16) for the
+//     lane's 2 elements (64 VGPRs);
+//   * clients stream in arrival order; each client's chunk is loaded once per wave (the four
+//     waves of a workgroup read the same 512 B, served by the CU's L1 / the XCD's L2, so HBM
+//     sees every client byte once per receiver group) and folded into 16 receivers x 2
+//     elements: 32 fp64 (mul, add) pairs per 8-byte load — VALU-bound, ~4 flop/byte;
+//   * the receiver's own update is excluded (:31-32) with a per-(client, wave) fold mask: the
+//     common case (no receiver of this wave excludes the client) is branch-free;
+//   * epilogue: divide by the receiver's per-segment total, store out_j, and fold the
+//     centralized average across the waves in receiver order through LDS (one barrier per
+//     wave); receivers beyond 64 run as further launches that carry the centralized chain
+//     in an fp64 scratch buffer.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fedavg_hip.h"
+
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_fail(int32_t code, const char* msg);
+
+namespace {
+
+int32_t pfail(int32_t code, const std::string& msg) { return fedavg_internal_fail(code, msg.c_str()); }
+
+#define PERS_HIP_TRY(expr)                                                                \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      return pfail(FEDAVG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+    }                                                                                     \
+  } while (0)
+
+#define PERS_RET(expr)              \
+  do {                              \
+    int32_t r_ = (expr);            \
+    if (r_ != FEDAVG_OK) return r_; \
+  } while (0)
+
+constexpr int kVE = 2;                 // elements per lane
+constexpr int kChunk = 64 * kVE;       // elements per workgroup
+constexpr int kJB = 16;                // receivers per wave
+constexpr int kMaxWaves = 8;           // waves per workgroup
+constexpr int kGroup = kMaxWaves * kJB;  // receivers per launch (128)
+constexpr int kU = 4;                  // clients loaded ahead per lane
+
+struct PChunk {
+  int32_t seg;
+  int32_t count;  // elements (== kChunk except at a segment's end)
+  int64_t start;  // first element, relative to the segment
+};
+
+enum CentralMode : int32_t {
+  CENTRAL_NONE = 0,
+  CENTRAL_FINAL = 1,     // fold this launch's receivers, write the centralized model
+  CENTRAL_CARRY_OUT = 2, // ... write the fp64 chain to the carry buffer (more groups follow)
+};
+
+struct PArgs {
+  const PChunk* chunks;
+  const void* const* cptrs;   // [T][Npad] segment-major client pointers (NULL = absent / padding)
+  const double* w;            // [Npad][waves*16] weights: receiver r of the launch at column r;
+                              // 0 for the pairs the reference skips (own update, absent, padding)
+  const int32_t* exmask;      // [N][waves] bit j: the wave's receiver j skips client k (own update)
+  const void* zeros;          // kChunk zero doubles (loads of absent tensors and padding)
+  const double* wtot;         // [kGroup][T] per-receiver, per-segment total weight
+  void* const* outs;          // [kGroup][T] output pointers
+  void* const* central;       // [T] centralized outputs (CENTRAL_FINAL)
+  double* carry;              // flat fp64 carry of the centralized chain (P elements)
+  const int64_t* seg_off;     // [T] segment offsets in the carry
+  uint32_t* flag;             // [0] acc NaN, [1] result NaN, [2] centralized NaN
+  int32_t N;                  // clients (arrivals)
+  int32_t Npad;               // N rounded up to the client group size kU
+  int32_t T;
+  int32_t aligned;            // every client / output pointer allows the vector accesses
+  int32_t M;                  // receivers of this launch (<= kGroup)
+  int32_t waves;              // waves of the launch (ceil(M / 16))
+  int32_t wstride;            // row stride of w (waves * 16)
+  int32_t out_f32;
+  int32_t central_mode;
+  int32_t central_in;         // 1 = continue the chain from the carry buffer
+  int32_t central_f32;
+  double cw;                  // 1 / (number of receivers), the weighted_avg weight
+};
+
+#define PERS_AS_GLOBAL __attribute__((address_space(1)))
+#define PERS_AS_CONST __attribute__((address_space(4)))
+template <typename T>
+using gp = T PERS_AS_GLOBAL*;
+template <typename T>
+using kp = const T PERS_AS_CONST*;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+struct bf16_t {
+  uint16_t bits;
+};
+
+__device__ __forceinline__ double h2d(uint32_t h) {
+  return static_cast<double>(__half2float(__ushort_as_half(static_cast<unsigned short>(h))));
+}
+__device__ __forceinline__ double b2d(uint32_t b) { return static_cast<double>(__uint_as_float(b << 16)); }
+
+// Raw (undecoded) 2-element slice of one client chunk for one lane: loaded one client group
+// ahead of the fold (software pipelining), expanded to doubles when folded.
+template <typename T>
+struct Raw;
+template <>
+struct Raw<float> {
+  using type = f32x2;
+  static constexpr int kSize = 4;
+  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const f32x2>)((gp<const float>)b + e)); }
+  __device__ __forceinline__ static type guarded(uint64_t b, int e, int count) {
+    type v;
+    v.x = (e < count) ? ((gp<const float>)b)[e] : 0.f;
+    v.y = (e + 1 < count) ? ((gp<const float>)b)[e + 1] : 0.f;
+    return v;
+  }
+  __device__ __forceinline__ static void expand(type v, double& x0, double& x1) {
+    x0 = v.x;
+    x1 = v.y;
+  }
+};
+template <>
+struct Raw<double> {
+  using type = f64x2;
+  static constexpr int kSize = 8;
+  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const f64x2>)((gp<const double>)b + e)); }
+  __device__ __forceinline__ static type guarded(uint64_t b, int e, int count) {
+    type v;
+    v.x = (e < count) ? ((gp<const double>)b)[e] : 0.0;
+    v.y = (e + 1 < count) ? ((gp<const double>)b)[e + 1] : 0.0;
+    return v;
+  }
+  __device__ __forceinline__ static void expand(type v, double& x0, double& x1) {
+    x0 = v.x;
+    x1 = v.y;
+  }
+};
+template <typename H>
+struct Raw16 {  // 2-byte inputs: both elements in one dword
+  using type = uint32_t;
+  static constexpr int kSize = 2;
+  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const uint32_t>)((gp<const uint16_t>)b + e)); }
+  __device__ __forceinline__ static type guarded(uint64_t b, int e, int count) {
+    const uint32_t lo = (e < count) ? ((gp<const uint16_t>)b)[e] : 0u;
+    const uint32_t hi = (e + 1 < count) ? ((gp<const uint16_t>)b)[e + 1] : 0u;
+    return lo | (hi << 16);
+  }
+  __device__ __forceinline__ static void expand(type v, double& x0, double& x1) {
+    x0 = H::cvt(v & 0xffffu);
+    x1 = H::cvt(v >> 16);
+  }
+};
+struct HalfCvt {
+  __device__ __forceinline__ static double cvt(uint32_t h) { return h2d(h); }
+};
+struct Bf16Cvt {
+  __device__ __forceinline__ static double cvt(uint32_t h) { return b2d(h); }
+};
+template <>
+struct Raw<__half> : Raw16<HalfCvt> {};
+template <>
+struct Raw<bf16_t> : Raw16<Bf16Cvt> {};
+
+enum PFold : int { PF_MULADD = 0, PF_FMA = 1 };
+
+template <int FOLD>
+__device__ __forceinline__ double pfold(double acc, double x, double w) {
+  if constexpr (FOLD == PF_FMA) {
+    return __builtin_fma(x, w, acc);  // exact products (host-proven): same rounding
+  } else {
+    const double p = x * w;  // tmp = x.to(float64) * w   (fed_avg_algorithm.py:54)
+    return acc + p;          // acc += tmp                 (:58)
+  }
+}
+
+__device__ __forceinline__ void pflag(uint32_t* flag, int word) {
+  __hip_atomic_store(flag + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Base address of client k's slice of this chunk: an absent tensor (NULL) or a padding client
+// reads the zero block instead (its weights are 0 for every receiver).
+__device__ __forceinline__ uint64_t client_base(uint64_t p, int64_t start_bytes, uint64_t zeros) {
+  return p ? p + start_bytes : zeros;
+}
+
+template <typename T, bool FULL>
+__device__ __forceinline__ typename Raw<T>::type load_raw(uint64_t b, int e, int count) {
+  if constexpr (FULL) {
+    return Raw<T>::full(b, e);
+  } else {
+    return Raw<T>::guarded(b, e, count);
+  }
+}
+
+// The main loop. Every receiver of the wave folds every client of the (padded) arrival list:
+// the pairs the reference skips — a receiver's own update (:31-32), an absent tensor, padding —
+// carry weight 0. Folding x*0 into acc is exact (acc + ±0 == acc) except when acc is -0.0 and
+// the product +0.0 (the sum becomes +0.0) or x is inf/NaN (the product is NaN); both leave a
+// receiver's final sum at ±0 or NaN, so those — and only those — elements are re-folded at the
+// end with the skipped pairs really skipped (refold below). The loop itself has no branches
+// and no per-receiver tests: 16 receivers x 2 elements fold per 8-byte load, with the next
+// client group's loads in flight.
+template <typename T, int FOLD, bool FULL>
+__device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, int seg, int count, int64_t start,
+                                          double* chain) {
+  using R = Raw<T>;
+  using RT = typename R::type;
+  const int j0 = wave * kJB;  // first receiver of this wave (within the launch)
+  const int e = lane * kVE;
+  const int64_t sb = start * R::kSize;
+  const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
+  const kp<uint64_t> ptrs = (kp<uint64_t>)(a.cptrs) + static_cast<int64_t>(seg) * a.Npad;
+  const kp<double> wt = (kp<double>)(a.w) + j0;
+
+  // fp64 accumulators of the wave's 16 receivers for the lane's two elements, started at the
+  // IEEE additive identity (-0.0 + p == p: the first fold equals the reference's assignment)
+  double acc0[kJB], acc1[kJB];
+#pragma unroll
+  for (int j = 0; j < kJB; ++j) acc0[j] = acc1[j] = -0.0;
+
+  RT nxt[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[u], sb, zeros), e, count);
+  for (int k = 0; k < a.Npad; k += kU) {
+    RT cur[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) cur[u] = nxt[u];
+    const int kn = (k + kU < a.Npad) ? k + kU : k;  // the last group re-loads itself (L2 hits)
+#pragma unroll
+    for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[kn + u], sb, zeros), e, count);
+    // keep the next group's loads ahead of this group's folds (the scheduler would otherwise
+    // sink them to the next iteration, next to their use)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      double x0, x1;
+      R::expand(cur[u], x0, x1);
+      const kp<double> wk = wt + static_cast<int64_t>(k + u) * a.wstride;
+#pragma unroll
+      for (int j = 0; j < kJB; ++j) {
+        const double wj = wk[j];
+        acc0[j] = pfold<FOLD>(acc0[j], x0, wj);
+        acc1[j] = pfold<FOLD>(acc1[j], x1, wj);
+      }
+    }
+  }
+
+  const bool in0 = e < count, in1 = e + 1 < count;
+  // refold (rare): elements whose sum is ±0 or NaN are recomputed with the skipped pairs
+  // skipped, giving the reference's exact sign of zero / its NaN-or-not verdict
+  bool fix = false;
+#pragma unroll
+  for (int j = 0; j < kJB; ++j)
+    fix |= (in0 && (acc0[j] == 0.0 || acc0[j] != acc0[j])) || (in1 && (acc1[j] == 0.0 || acc1[j] != acc1[j]));
+  if (__ballot(fix) != 0ull) {
+    double b0[kJB], b1[kJB];
+#pragma unroll
+    for (int j = 0; j < kJB; ++j) b0[j] = b1[j] = -0.0;
+    const kp<int32_t> exm = (kp<int32_t>)(a.exmask);
+    for (int k = 0; k < a.N; ++k) {
+      const uint64_t p = ptrs[k];
+      if (!p) continue;  // absent tensor: nobody folds it
+      const uint32_t em = static_cast<uint32_t>(exm[static_cast<int64_t>(k) * a.waves + wave]);
+      double x0, x1;
+      R::expand(load_raw<T, FULL>(p + sb, e, count), x0, x1);
+      const kp<double> wk = wt + static_cast<int64_t>(k) * a.wstride;
+#pragma unroll
+      for (int j = 0; j < kJB; ++j) {
+        if ((em >> j) & 1u) continue;  // receiver j's own update
+        b0[j] = pfold<FOLD>(b0[j], x0, wk[j]);
+        b1[j] = pfold<FOLD>(b1[j], x1, wk[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kJB; ++j) {
+      if (acc0[j] == 0.0 || acc0[j] != acc0[j]) acc0[j] = b0[j];
+      if (acc1[j] == 0.0 || acc1[j] != acc1[j]) acc1[j] = b1[j];
+    }
+  }
+
+  // epilogue: out_j = acc_j / W_j with the fused NaN assertions (fed_avg_algorithm.py:92-97)
+  bool bad_acc = false, bad_res = false;
+  const kp<double> wtot = (kp<double>)(a.wtot);
+  const kp<uint64_t> outs = (kp<uint64_t>)(a.outs);
+  double r0[kJB], r1[kJB];
+#pragma unroll
+  for (int j = 0; j < kJB; ++j) {
+    r0[j] = acc0[j];
+    r1[j] = acc1[j];
+    if (j0 + j >= a.M) continue;  // (continue, not break: keeps the loop fully unrolled)
+    const double W = wtot[static_cast<int64_t>(j0 + j) * a.T + seg];
+    bad_acc |= (in0 && r0[j] != r0[j]) || (in1 && r1[j] != r1[j]);
+    r0[j] = r0[j] / W;
+    r1[j] = r1[j] / W;
+    bad_res |= (in0 && r0[j] != r0[j]) || (in1 && r1[j] != r1[j]);
+    const uint64_t op = outs[static_cast<int64_t>(j0 + j) * a.T + seg];
+    if (a.out_f32) {
+      gp<float> o = (gp<float>)(reinterpret_cast<void*>(op)) + start + e;
+      if (FULL) {
+        __builtin_nontemporal_store(f32x2{static_cast<float>(r0[j]), static_cast<float>(r1[j])}, (gp<f32x2>)o);
+      } else {
+        if (in0) o[0] = static_cast<float>(r0[j]);
+        if (in1) o[1] = static_cast<float>(r1[j]);
+      }
+    } else {
+      gp<double> o = (gp<double>)(reinterpret_cast<void*>(op)) + start + e;
+      if (FULL) {
+        __builtin_nontemporal_store(f64x2{r0[j], r1[j]}, (gp<f64x2>)o);
+      } else {
+        if (in0) o[0] = r0[j];
+        if (in1) o[1] = r1[j];
+      }
+    }
+  }
+  if (__ballot(bad_acc) != 0ull && lane == 0) pflag(a.flag, 0);
+  if (__ballot(bad_res) != 0ull && lane == 0) pflag(a.flag, 1);
+  if (a.central_mode == CENTRAL_NONE) return;
+
+  // centralized model: fold round(out_j * cw) over receivers in key order; wave w continues
+  // the chain of wave w-1 through LDS (weighted_avg, aggregation_algorithm.py:63-72)
+  const int64_t coff = a.seg_off[seg] + start + e;
+  for (int s = 0; s < a.waves; ++s) {
+    if (wave == s) {
+      double c0, c1;
+      if (s > 0) {
+        c0 = chain[lane * kVE];
+        c1 = chain[lane * kVE + 1];
+      } else if (a.central_in) {
+        c0 = in0 ? a.carry[coff] : -0.0;
+        c1 = in1 ? a.carry[coff + 1] : -0.0;
+      } else {
+        c0 = c1 = -0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < kJB; ++j) {
+        if (j0 + j >= a.M) continue;
+        const double d0 = r0[j] * a.cw;  // v.to(float64) * weight   (:65-68)
+        const double d1 = r1[j] * a.cw;
+        c0 = c0 + d0;                    // avg_data[k] += d[k]       (:72)
+        c1 = c1 + d1;
+      }
+      if (s + 1 < a.waves) {
+        chain[lane * kVE] = c0;
+        chain[lane * kVE + 1] = c1;
+      } else if (a.central_mode == CENTRAL_CARRY_OUT) {
+        if (in0) a.carry[coff] = c0;
+        if (in1) a.carry[coff + 1] = c1;
+      } else {
+        const bool bad = (in0 && c0 != c0) || (in1 && c1 != c1);  // (:73-74)
+        if (__ballot(bad) != 0ull && lane == 0) pflag(a.flag, 2);
+        const uint64_t op = ((kp<uint64_t>)(a.central))[seg];
+        if (a.central_f32) {
+          gp<float> o = (gp<float>)(reinterpret_cast<void*>(op)) + start + e;
+          if (in0) o[0] = static_cast<float>(c0);
+          if (in1) o[1] = static_cast<float>(c1);
+        } else {
+          gp<double> o = (gp<double>)(reinterpret_cast<void*>(op)) + start + e;
+          if (in0) o[0] = c0;
+          if (in1) o[1] = c1;
+        }
+      }
+    }
+    if (s + 1 < a.waves) __syncthreads();
+  }
+}
+
+template <typename T, int FOLD>
+__global__ __launch_bounds__(64 * kMaxWaves) void personalized_kernel(PArgs a) {
+  __shared__ double chain[64 * kVE];
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  const kp<int32_t> cd = (kp<int32_t>)(a.chunks + blockIdx.x);
+  const int seg = cd[0];
+  const int count = cd[1];
+  const int64_t start = ((kp<int64_t>)(a.chunks + blockIdx.x))[1];
+  if (count == kChunk && a.aligned) {
+    pers_body<T, FOLD, true>(a, wave, lane, seg, count, start, chain);
+  } else {
+    pers_body<T, FOLD, false>(a, wave, lane, seg, count, start, chain);
+  }
+}
+
+// fp64 VALU ceiling probe (the roofline this kernel is priced against): every lane runs
+// `iters` dependent-free chains of v_fma_f64.
+__global__ __launch_bounds__(256) void fp64_fma_probe(double* out, int iters) {
+  double a0 = threadIdx.x * 1e-9, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
+         a6 = a0 + 6, a7 = a0 + 7;
+  const double m = 0.999999, c = 1e-7;
+  for (int i = 0; i < iters; ++i) {
+    a0 = __builtin_fma(a0, m, c); a1 = __builtin_fma(a1, m, c); a2 = __builtin_fma(a2, m, c);
+    a3 = __builtin_fma(a3, m, c); a4 = __builtin_fma(a4, m, c); a5 = __builtin_fma(a5, m, c);
+    a6 = __builtin_fma(a6, m, c); a7 = __builtin_fma(a7, m, c);
+  }
+  const double s = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+  if (s == 12345.678) out[blockIdx.x] = s;  // keeps the chains live
+}
+
+int32_t elem_size(int32_t dt) {
+  switch (dt) {
+    case FEDAVG_F32: return 4;
+    case FEDAVG_F16: return 2;
+    case FEDAVG_BF16: return 2;
+    case FEDAVG_F64: return 8;
+    default: return 0;
+  }
+}
+
+int32_t sig_bits(int32_t dt) {
+  switch (dt) {
+    case FEDAVG_F32: return 24;
+    case FEDAVG_F16: return 11;
+    case FEDAVG_BF16: return 8;
+    default: return 53;
+  }
+}
+
+// Significand width of a weight; -1 when a product with it could over/underflow or is not
+// finite (then the separately rounded fold is used).
+int weight_bits(double w) {
+  if (w == 0.0) return 0;
+  if (!std::isfinite(w)) return -1;
+  int ex = 0;
+  const double m = std::frexp(std::fabs(w), &ex);
+  if (ex < -800 || ex > 800) return -1;
+  const uint64_t bits = static_cast<uint64_t>(std::ldexp(m, 53));
+  return 53 - __builtin_ctzll(bits);
+}
+
+constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct fedavg_pers {
+  int device = 0;
+  int T = 0;
+  std::vector<int64_t> seg_numel, seg_off;
+  int64_t P = 0;
+  std::vector<PChunk> chunks;
+  PChunk* d_chunks = nullptr;
+  int64_t* d_seg_off = nullptr;
+  double* d_carry = nullptr;
+  uint32_t* h_flag = nullptr;
+  uint32_t* d_flag = nullptr;
+  // per-call table staging: pinned host image + device copy, reused once the previous
+  // call's copy has completed
+  char* h_blob = nullptr;
+  char* d_blob = nullptr;
+  size_t blob_cap = 0;
+  hipEvent_t blob_done = nullptr;
+  bool blob_used = false;
+  bool allow_fma = true;
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+};
+
+namespace {
+
+template <typename T>
+hipError_t launch_pers_t(const PArgs& a, int fold, int nchunks, int threads, hipStream_t s) {
+  if (fold == PF_FMA) {
+    hipLaunchKernelGGL((personalized_kernel<T, PF_FMA>), dim3(nchunks), dim3(threads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((personalized_kernel<T, PF_MULADD>), dim3(nchunks), dim3(threads), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pers(int32_t dt, const PArgs& a, int fold, int nchunks, int threads, hipStream_t s) {
+  switch (dt) {
+    case FEDAVG_F32: return launch_pers_t<float>(a, fold, nchunks, threads, s);
+    case FEDAVG_F16: return launch_pers_t<__half>(a, fold, nchunks, threads, s);
+    case FEDAVG_BF16: return launch_pers_t<bf16_t>(a, fold, nchunks, threads, s);
+    case FEDAVG_F64: return launch_pers_t<double>(a, fold, nchunks, threads, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int32_t check_pers(const fedavg_pers* p) {
+  if (p == nullptr) return pfail(FEDAVG_ERR_INVALID, "null personalized context");
+  return FEDAVG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t fedavg_pers_create(fedavg_pers** out, int32_t device, const int64_t* seg_numel, int32_t num_segments) {
+  if (out == nullptr) return pfail(FEDAVG_ERR_INVALID, "null out");
+  *out = nullptr;
+  if (num_segments <= 0 || seg_numel == nullptr) return pfail(FEDAVG_ERR_INVALID, "no segments");
+  for (int t = 0; t < num_segments; ++t)
+    if (seg_numel[t] <= 0 || seg_numel[t] > (int64_t(1) << 40))
+      return pfail(FEDAVG_ERR_INVALID, "bad segment size");
+  PERS_HIP_TRY(hipSetDevice(device));
+  fedavg_pers* p = new fedavg_pers();
+  p->device = device;
+  p->T = num_segments;
+  p->seg_numel.assign(seg_numel, seg_numel + num_segments);
+  p->seg_off.resize(num_segments);
+  for (int t = 0; t < num_segments; ++t) {
+    p->seg_off[t] = p->P;
+    p->P += seg_numel[t];
+    for (int64_t s = 0; s < seg_numel[t]; s += kChunk)
+      p->chunks.push_back(PChunk{t, static_cast<int32_t>(std::min<int64_t>(kChunk, seg_numel[t] - s)), s});
+  }
+  if (p->chunks.size() > static_cast<size_t>(INT32_MAX)) {
+    delete p;
+    return pfail(FEDAVG_ERR_INVALID, "layout too large");
+  }
+  auto cleanup = [&](hipError_t e, const char* what) {
+    fedavg_pers_destroy(p);
+    return pfail(FEDAVG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_chunks), sizeof(PChunk) * p->chunks.size())) != hipSuccess)
+    return cleanup(e, "hipMalloc chunks");
+  if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_seg_off), sizeof(int64_t) * num_segments)) != hipSuccess)
+    return cleanup(e, "hipMalloc seg_off");
+  if ((e = hipMemcpy(p->d_chunks, p->chunks.data(), sizeof(PChunk) * p->chunks.size(), hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "hipMemcpy chunks");
+  if ((e = hipMemcpy(p->d_seg_off, p->seg_off.data(), sizeof(int64_t) * num_segments, hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "hipMemcpy seg_off");
+  if ((e = hipHostMalloc(reinterpret_cast<void**>(&p->h_flag), sizeof(uint32_t) * 4,
+                         hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return cleanup(e, "hipHostMalloc flag");
+  if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_flag), p->h_flag, 0)) != hipSuccess)
+    return cleanup(e, "hipHostGetDevicePointer flag");
+  std::memset(p->h_flag, 0, sizeof(uint32_t) * 4);
+  if ((e = hipEventCreateWithFlags(&p->blob_done, hipEventDisableTiming)) != hipSuccess)
+    return cleanup(e, "hipEventCreate");
+  *out = p;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_pers_destroy(fedavg_pers* p) {
+  if (p == nullptr) return FEDAVG_OK;
+  (void)hipSetDevice(p->device);
+  (void)hipDeviceSynchronize();
+  for (auto& pr : p->prof_events) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (p->blob_done) (void)hipEventDestroy(p->blob_done);
+  if (p->h_blob) (void)hipHostFree(p->h_blob);
+  if (p->d_blob) (void)hipFree(p->d_blob);
+  if (p->d_chunks) (void)hipFree(p->d_chunks);
+  if (p->d_seg_off) (void)hipFree(p->d_seg_off);
+  if (p->d_carry) (void)hipFree(p->d_carry);
+  if (p->h_flag) (void)hipHostFree(p->h_flag);
+  delete p;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_pers_set_fused_fold(fedavg_pers* p, int32_t enable) {
+  PERS_RET(check_pers(p));
+  p->allow_fma = enable != 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, int32_t in_dtype, int32_t N,
+                              const int64_t* client_ids, const double* weights, const int64_t* receiver_ids,
+                              int32_t M, void* const* out_ptrs, int32_t out_dtype, void* const* central_ptrs,
+                              int32_t central_dtype, void* stream) {
+  PERS_RET(check_pers(p));
+  const int T = p->T;
+  if (N <= 0 || M <= 0) return pfail(FEDAVG_ERR_INVALID, "need at least one client and one receiver");
+  if (!client_ptrs || !client_ids || !weights || !receiver_ids || !out_ptrs)
+    return pfail(FEDAVG_ERR_INVALID, "null table");
+  if (elem_size(in_dtype) == 0) return pfail(FEDAVG_ERR_INVALID, "bad input dtype");
+  if (out_dtype != FEDAVG_F32 && out_dtype != FEDAVG_F64)
+    return pfail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (central_ptrs && central_dtype != FEDAVG_F32 && central_dtype != FEDAVG_F64)
+    return pfail(FEDAVG_ERR_INVALID, "central dtype must be FEDAVG_F32 or FEDAVG_F64");
+  for (int j = 0; j < M; ++j)
+    for (int i = 0; i < j; ++i)
+      if (receiver_ids[i] == receiver_ids[j]) return pfail(FEDAVG_ERR_INVALID, "duplicate receiver id");
+  bool aligned = true;
+  const size_t in_align = static_cast<size_t>(elem_size(in_dtype)) * kVE;
+  for (int64_t i = 0; i < static_cast<int64_t>(M) * T; ++i) {
+    if (!out_ptrs[i]) return pfail(FEDAVG_ERR_INVALID, "null output pointer");
+    if (reinterpret_cast<uintptr_t>(out_ptrs[i]) % (out_dtype == FEDAVG_F64 ? 16 : 8) != 0) aligned = false;
+  }
+  for (int64_t i = 0; i < static_cast<int64_t>(N) * T; ++i)
+    if (client_ptrs[i] && reinterpret_cast<uintptr_t>(client_ptrs[i]) % in_align != 0) aligned = false;
+  if (central_ptrs)
+    for (int t = 0; t < T; ++t)
+      if (!central_ptrs[t]) return pfail(FEDAVG_ERR_INVALID, "null centralized output pointer");
+
+  // receiver j folds arrival k unless it is j's own update (:31-32); per-receiver, per-segment
+  // totals in arrival order (fed_avg_algorithm.py:59-62); the fused-fold proof (every folded
+  // product exact in fp64)
+  std::vector<int32_t> excl(N, -1);  // the receiver that skips arrival k (ids are unique)
+  for (int k = 0; k < N; ++k)
+    for (int j = 0; j < M; ++j)
+      if (receiver_ids[j] == client_ids[k]) excl[k] = j;
+  std::vector<double> wtot(static_cast<size_t>(M) * T, 0.0);
+  std::vector<uint8_t> have(static_cast<size_t>(M) * T, 0);
+  int max_bits = 0;
+  bool tame = true;
+  for (int k = 0; k < N; ++k) {
+    for (int j = 0; j < M; ++j) {
+      if (excl[k] == j) continue;
+      const double w = weights[static_cast<int64_t>(j) * N + k];
+      const int b = weight_bits(w);
+      if (b < 0) tame = false;
+      max_bits = std::max(max_bits, b);
+      for (int t = 0; t < T; ++t) {
+        if (!client_ptrs[static_cast<int64_t>(k) * T + t]) continue;
+        wtot[static_cast<size_t>(j) * T + t] += w;
+        have[static_cast<size_t>(j) * T + t] = 1;
+      }
+    }
+  }
+  for (int j = 0; j < M; ++j)
+    for (int t = 0; t < T; ++t)
+      if (!have[static_cast<size_t>(j) * T + t])
+        return pfail(FEDAVG_ERR_STATE, "receiver " + std::to_string(j) + " has no data for segment " +
+                                           std::to_string(t) + " (fed_avg_algorithm.py:88)");
+  const int fold = (p->allow_fma && tame && sig_bits(in_dtype) + max_bits <= 53) ? PF_FMA : PF_MULADD;
+
+  // one blob: [T][Npad] pointers; per receiver group g: [Npad][waves*16] weights, [N][waves]
+  // skip masks, [kGroup][T] totals, [kGroup][T] outputs; then [T] centralized outputs and
+  // the zero block
+  const int G = (M + kGroup - 1) / kGroup;
+  const int Npad = (N + kU - 1) / kU * kU;
+  const size_t off_ptr = 0;
+  const size_t sz_ptr = align_up(sizeof(void*) * T * Npad, 256);
+  const size_t sz_w = align_up(sizeof(double) * Npad * kGroup, 256);
+  const size_t sz_x = align_up(sizeof(int32_t) * N * kMaxWaves, 256);
+  const size_t sz_t = align_up(sizeof(double) * kGroup * T, 256);
+  const size_t sz_o = align_up(sizeof(void*) * kGroup * T, 256);
+  const size_t per_g = sz_w + sz_x + sz_t + sz_o;
+  const size_t off_g = off_ptr + sz_ptr;
+  const size_t off_c = off_g + per_g * G;
+  const size_t off_z = off_c + align_up(sizeof(void*) * T, 256);
+  const size_t bytes = off_z + sizeof(double) * kChunk;
+
+  PERS_HIP_TRY(hipSetDevice(p->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->blob_used) PERS_HIP_TRY(hipEventSynchronize(p->blob_done));
+  if (p->blob_cap < bytes) {
+    if (p->h_blob) PERS_HIP_TRY(hipHostFree(p->h_blob));
+    if (p->d_blob) {
+      PERS_HIP_TRY(hipStreamSynchronize(s));
+      PERS_HIP_TRY(hipFree(p->d_blob));
+    }
+    p->h_blob = nullptr;
+    p->d_blob = nullptr;
+    p->blob_cap = 0;
+    const size_t cap = std::max<size_t>(bytes * 2, 64 * 1024);
+    PERS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p->h_blob), cap, hipHostMallocDefault));
+    PERS_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_blob), cap));
+    p->blob_cap = cap;
+  }
+  char* h = p->h_blob;
+  std::memset(h, 0, bytes);
+  const void** hp = reinterpret_cast<const void**>(h + off_ptr);
+  for (int t = 0; t < T; ++t)
+    for (int k = 0; k < N; ++k) hp[static_cast<size_t>(t) * Npad + k] = client_ptrs[static_cast<int64_t>(k) * T + t];
+  for (int g = 0; g < G; ++g) {
+    char* b = h + off_g + per_g * g;
+    double* hw = reinterpret_cast<double*>(b);
+    int32_t* hx = reinterpret_cast<int32_t*>(b + sz_w);
+    double* ht = reinterpret_cast<double*>(b + sz_w + sz_x);
+    void** ho = reinterpret_cast<void**>(b + sz_w + sz_x + sz_t);
+    const int Mg = std::min(kGroup, M - g * kGroup);
+    const int waves = (Mg + kJB - 1) / kJB;
+    const int wstride = kJB * waves;
+    for (int k = 0; k < N; ++k) {
+      for (int r = 0; r < Mg; ++r) {
+        const int j = g * kGroup + r;
+        if (excl[k] == j) {
+          hx[static_cast<size_t>(k) * waves + r / kJB] |= 1 << (r % kJB);  // weight stays 0
+        } else {
+          hw[static_cast<size_t>(k) * wstride + r] = weights[static_cast<int64_t>(j) * N + k];
+        }
+      }
+    }
+    for (int r = 0; r < Mg; ++r)
+      for (int t = 0; t < T; ++t) {
+        const int j = g * kGroup + r;
+        ht[static_cast<size_t>(r) * T + t] = wtot[static_cast<size_t>(j) * T + t];
+        ho[static_cast<size_t>(r) * T + t] = out_ptrs[static_cast<int64_t>(j) * T + t];
+      }
+  }
+  if (central_ptrs) {
+    void** hc = reinterpret_cast<void**>(h + off_c);
+    for (int t = 0; t < T; ++t) hc[t] = central_ptrs[t];
+  }
+  PERS_HIP_TRY(hipMemcpyAsync(p->d_blob, h, bytes, hipMemcpyHostToDevice, s));
+  PERS_HIP_TRY(hipEventRecord(p->blob_done, s));
+  p->blob_used = true;
+  if (central_ptrs && G > 1 && !p->d_carry)
+    PERS_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_carry), sizeof(double) * p->P));
+
+  const int nchunks = static_cast<int>(p->chunks.size());
+  for (int g = 0; g < G; ++g) {
+    char* b = p->d_blob + off_g + per_g * g;
+    PArgs a;
+    a.chunks = p->d_chunks;
+    a.cptrs = reinterpret_cast<const void* const*>(p->d_blob + off_ptr);
+    a.w = reinterpret_cast<const double*>(b);
+    a.exmask = reinterpret_cast<const int32_t*>(b + sz_w);
+    a.wtot = reinterpret_cast<const double*>(b + sz_w + sz_x);
+    a.outs = reinterpret_cast<void* const*>(b + sz_w + sz_x + sz_t);
+    a.central = reinterpret_cast<void* const*>(p->d_blob + off_c);
+    a.zeros = p->d_blob + off_z;
+    a.carry = p->d_carry;
+    a.seg_off = p->d_seg_off;
+    a.flag = p->d_flag;
+    a.N = N;
+    a.Npad = Npad;
+    a.T = T;
+    a.aligned = aligned;
+    a.M = std::min(kGroup, M - g * kGroup);
+    a.waves = (a.M + kJB - 1) / kJB;
+    a.wstride = kJB * a.waves;
+    a.out_f32 = out_dtype == FEDAVG_F32;
+    a.central_mode = !central_ptrs ? CENTRAL_NONE : (g + 1 < G ? CENTRAL_CARRY_OUT : CENTRAL_FINAL);
+    a.central_in = g > 0;
+    a.central_f32 = central_dtype == FEDAVG_F32;
+    a.cw = 1.0 / static_cast<double>(M);
+    const int threads = 64 * a.waves;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (p->prof) {
+      PERS_HIP_TRY(hipEventCreate(&e0));
+      PERS_HIP_TRY(hipEventCreate(&e1));
+      PERS_HIP_TRY(hipEventRecord(e0, s));
+    }
+    const hipError_t err = launch_pers(in_dtype, a, fold, nchunks, threads, s);
+    if (err != hipSuccess) return pfail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
+    if (p->prof) {
+      PERS_HIP_TRY(hipEventRecord(e1, s));
+      p->prof_events.emplace_back(e0, e1);
+    }
+  }
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_pers_check(fedavg_pers* p, void* stream, uint32_t* flags_out) {
+  PERS_RET(check_pers(p));
+  PERS_HIP_TRY(hipSetDevice(p->device));
+  PERS_HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  uint32_t f = 0;
+  if (__atomic_load_n(&p->h_flag[0], __ATOMIC_ACQUIRE)) f |= FEDAVG_FLAG_ACC_NAN;
+  if (__atomic_load_n(&p->h_flag[1], __ATOMIC_ACQUIRE)) f |= FEDAVG_FLAG_RESULT_NAN;
+  if (__atomic_load_n(&p->h_flag[2], __ATOMIC_ACQUIRE)) f |= FEDAVG_FLAG_CENTRAL_NAN;
+  std::memset(p->h_flag, 0, sizeof(uint32_t) * 4);
+  if (flags_out) *flags_out = f;
+  if (f & FEDAVG_FLAG_ACC_NAN) return pfail(FEDAVG_ERR_NAN_ACCUM, "NaN in a receiver's accumulator");
+  if (f & FEDAVG_FLAG_RESULT_NAN) return pfail(FEDAVG_ERR_NAN_RESULT, "NaN in a receiver's result");
+  if (f & FEDAVG_FLAG_CENTRAL_NAN) return pfail(FEDAVG_ERR_NAN_RESULT, "NaN in the centralized model");
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_pers_prof_enable(fedavg_pers* p, int32_t enable) {
+  PERS_RET(check_pers(p));
+  p->prof = enable != 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_pers_prof_collect(fedavg_pers* p, double* total_ms, int32_t* launches) {
+  PERS_RET(check_pers(p));
+  double sum = 0.0;
+  for (auto& pr : p->prof_events) {
+    PERS_HIP_TRY(hipEventSynchronize(pr.second));
+    float ms = 0.f;
+    PERS_HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    sum += ms;
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (total_ms) *total_ms = sum;
+  if (launches) *launches = static_cast<int32_t>(p->prof_events.size());
+  p->prof_events.clear();
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_fp64_probe(int64_t waves, int32_t iters, double* tflops_out, void* stream) {
+  if (waves <= 0 || iters <= 0 || !tflops_out) return pfail(FEDAVG_ERR_INVALID, "bad probe arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  double* d = nullptr;
+  const int blocks = static_cast<int>((waves + 3) / 4);
+  PERS_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), sizeof(double) * blocks));
+  hipEvent_t e0, e1;
+  PERS_HIP_TRY(hipEventCreate(&e0));
+  PERS_HIP_TRY(hipEventCreate(&e1));
+  hipLaunchKernelGGL(fp64_fma_probe, dim3(blocks), dim3(256), 0, s, d, iters);  // warm-up
+  PERS_HIP_TRY(hipEventRecord(e0, s));
+  hipLaunchKernelGGL(fp64_fma_probe, dim3(blocks), dim3(256), 0, s, d, iters);
+  PERS_HIP_TRY(hipEventRecord(e1, s));
+  PERS_HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  PERS_HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(d);
+  *tflops_out = 2.0 * 8.0 * static_cast<double>(iters) * 256.0 * blocks / (ms * 1e-3) / 1e12;
+  return FEDAVG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""Host-side handle on the PersonalizedFedAVG kernel (``fedavg_pers_*`` of include/fedavg_hip.h).
+
+One ``PersonalizedContext`` per (layout, device). ``aggregate`` launches the whole round of
+the reference's ``PersonalizedFedAVGAlgorithm`` (personalized_aggregation_algorithm.py:23-57)
+— M per-receiver FedAvgs over N arrivals plus the centralized average — asynchronously on the
+current torch stream; ``check`` drains the stream and reports the fused NaN assertions.
+The arithmetic runs in ``csrc/personalized_kernels.hip``; there is no CPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from collections.abc import Sequence
+
+import numpy as np
+import torch
+
+from . import _native
+from .fedavg import ModelLayout, dtype_code, out_code
+
+_PTR = ctypes.POINTER(ctypes.c_void_p)
+_DBL = ctypes.POINTER(ctypes.c_double)
+_I64 = ctypes.POINTER(ctypes.c_int64)
+
+
+class PersonalizedContext:
+    def __init__(self, layout: ModelLayout, device: torch.device | str | int | None = None) -> None:
+        self._lib = _native.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("the personalized HIP path runs on a GPU device")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if layout.num_segments == 0 or min(layout.numels) <= 0:
+            raise ValueError("a native layout needs at least one tensor and no empty tensors")
+        self.device = device
+        self.layout = layout
+        numels = (ctypes.c_int64 * layout.num_segments)(*layout.numels)
+        handle = ctypes.c_void_p()
+        _native.check(self._lib.fedavg_pers_create(ctypes.byref(handle), device.index, numels, layout.num_segments))
+        self._h = handle
+        self._keep: tuple = ()
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.fedavg_pers_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self) -> None:  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> ctypes.c_void_p:
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def set_fused_fold(self, enable: bool) -> None:
+        _native.check(self._lib.fedavg_pers_set_fused_fold(self._h, 1 if enable else 0))
+
+    def aggregate(
+        self,
+        clients: Sequence[Sequence[torch.Tensor | None]],
+        in_dtype: torch.dtype,
+        client_ids: Sequence[int],
+        weights: np.ndarray,
+        receiver_ids: Sequence[int],
+        outs: Sequence[Sequence[torch.Tensor]],
+        out_dtype: torch.dtype,
+        central: Sequence[torch.Tensor] | None = None,
+        central_dtype: torch.dtype = torch.float64,
+    ) -> None:
+        """clients[N][T] (None = tensor not sent), weights[M][N] (float64), outs[M][T]."""
+        T = self.layout.num_segments
+        N, M = len(clients), len(receiver_ids)
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        if w.shape != (M, N) or len(client_ids) != N or len(outs) != M:
+            raise ValueError("clients, weights, ids and outputs disagree on N / M")
+        numels = self.layout.numels
+        ptrs = np.zeros(N * T, dtype=np.uint64)
+        keep: list[torch.Tensor] = []
+        for k, row in enumerate(clients):
+            if len(row) != T:
+                raise ValueError("client row does not match the layout")
+            for t, x in enumerate(row):
+                if x is None:
+                    continue
+                if x.device != self.device or x.dtype != in_dtype or x.numel() != numels[t] or not x.is_contiguous():
+                    raise ValueError("client tensors must be contiguous, on the device, of the input dtype and size")
+                ptrs[k * T + t] = x.data_ptr()
+                keep.append(x)
+        optrs = np.zeros(M * T, dtype=np.uint64)
+        for j, row in enumerate(outs):
+            for t, o in enumerate(row):
+                if o.device != self.device or o.dtype != out_dtype or o.numel() != numels[t] or not o.is_contiguous():
+                    raise ValueError("output tensors must be contiguous, on the device, of the output dtype and size")
+                optrs[j * T + t] = o.data_ptr()
+                keep.append(o)
+        cptrs = None
+        if central is not None:
+            cp = np.zeros(T, dtype=np.uint64)
+            for t, o in enumerate(central):
+                if o.device != self.device or o.dtype != central_dtype or o.numel() != numels[t] or not o.is_contiguous():
+                    raise ValueError("centralized outputs must be contiguous, on the device, of the dtype and size")
+                cp[t] = o.data_ptr()
+                keep.append(o)
+            cptrs = cp
+        cid = np.asarray(client_ids, dtype=np.int64)
+        rid = np.asarray(receiver_ids, dtype=np.int64)
+        self._keep = (ptrs, optrs, cptrs, cid, rid, w, keep)
+        _native.check(
+            self._lib.fedavg_pers_aggregate(
+                self._h, ptrs.ctypes.data_as(_PTR), dtype_code(in_dtype), N, cid.ctypes.data_as(_I64),
+                w.ctypes.data_as(_DBL), rid.ctypes.data_as(_I64), M, optrs.ctypes.data_as(_PTR),
+                out_code(out_dtype), None if cptrs is None else cptrs.ctypes.data_as(_PTR),
+                out_code(central_dtype), self.stream,
+            )
+        )
+
+    def check(self) -> int:
+        """Drain the stream; returns the NaN flag bits (FLAG_ACC_NAN / RESULT / CENTRAL) and clears them."""
+        flags = ctypes.c_uint32()
+        self._lib.fedavg_pers_check(self._h, self.stream, ctypes.byref(flags))
+        return int(flags.value)
+
+    def prof_enable(self, on: bool = True) -> None:
+        _native.check(self._lib.fedavg_pers_prof_enable(self._h, 1 if on else 0))
+
+    def prof_collect(self) -> tuple[float, int]:
+        ms, n = ctypes.c_double(), ctypes.c_int32()
+        _native.check(self._lib.fedavg_pers_prof_collect(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+def fp64_probe(device: torch.device, waves: int = 256 * 4 * 8, iters: int = 4096) -> float:
+    """Measured fp64 VALU ceiling (TFLOP/s) of independent v_fma_f64 chains."""
+    lib = _native.load()
+    out = ctypes.c_double()
+    with torch.cuda.device(device):
+        _native.check(lib.fedavg_fp64_probe(waves, iters, ctypes.byref(out),
+                                            ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)))
+    return out.value

@@ -72,6 +72,7 @@ enum fedavg_status {
 /* flag bits latched by the kernels (read through fedavg_check) */
 #define FEDAVG_FLAG_ACC_NAN 0x1u
 #define FEDAVG_FLAG_RESULT_NAN 0x2u
+#define FEDAVG_FLAG_CENTRAL_NAN 0x4u /* personalized path: the centralized average */
 
 typedef struct fedavg_ctx fedavg_ctx;
 
@@ -235,6 +236,46 @@ int32_t fedavg_prof_collect(fedavg_ctx* ctx, double* total_ms, int32_t* launches
 /* HBM ceiling probes (bench.py's measured copy / read roofline): mode 0 = 16-B copy of
  * `bytes` from src to dst, mode 1 = 16-B read-only stream of src (dst: >= 8 KiB scratch). */
 int32_t fedavg_bw_probe(const void* src, int64_t bytes, void* dst, int32_t mode, void* stream);
+
+/* =====================================================================================
+ * PersonalizedFedAVG (simulation_lib/algorithm/personalized_aggregation_algorithm.py:9-57)
+ *
+ * Every receiver j keeps its own FedAvg over the other workers' updates, weighted by
+ * worker_weights[j].get(i, 0) (:23-43); the centralized model is the equal-weight average of
+ * the receivers' results in receiver order (:45-57 -> aggregation_algorithm.py:51-76).
+ * One call replaces the whole round: N arrivals x M receivers, all client buckets resident.
+ *
+ *  client_ptrs[N][T]  arrival-ordered client tensors (NULL = the client did not send tensor t)
+ *  client_ids[N]      worker id of each arrival
+ *  weights[M][N]      receiver j's weight for arrival k (the .get(i, 0) value)
+ *  receiver_ids[M]    worker id of each receiver (unique; receiver order = key order): receiver
+ *                     j skips the arrivals whose id equals its own (:31-32)
+ *  out_ptrs[M][T]     receiver results: acc_j / W_j (fed_avg_algorithm.py:71-99), fp32 or fp64
+ *  central_ptrs[T]    optional: sum_j round(out_j * (1/M)) in receiver order, fp32 or fp64
+ * Per receiver and segment the sum is the reference's arrival-order fp64 chain with separately
+ * rounded products (fused to one fma only when the host proves every product exact), so every
+ * output is bit-identical to the reference's float64 result (the fp32 outputs: its cast).
+ * FEDAVG_ERR_STATE when a receiver folds no client for some segment (the :88 assertion). NaN
+ * conditions (input NaN, inf*0, 0/0, inf-inf) latch flags reported by fedavg_pers_check.
+ * ===================================================================================== */
+typedef struct fedavg_pers fedavg_pers;
+int32_t fedavg_pers_create(fedavg_pers** out, int32_t device, const int64_t* seg_numel, int32_t num_segments);
+int32_t fedavg_pers_destroy(fedavg_pers* p);
+/* fused fold when every product is provably exact (default on; results identical either way) */
+int32_t fedavg_pers_set_fused_fold(fedavg_pers* p, int32_t enable);
+int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, int32_t in_dtype,
+                              int32_t num_clients, const int64_t* client_ids, const double* weights,
+                              const int64_t* receiver_ids, int32_t num_receivers,
+                              void* const* out_ptrs, int32_t out_dtype, void* const* central_ptrs,
+                              int32_t central_dtype, void* stream);
+/* Synchronise `stream`, report and clear the NaN flags (FEDAVG_FLAG_*): FEDAVG_OK,
+ * FEDAVG_ERR_NAN_ACCUM (a receiver's accumulator: input NaN, inf*0, inf-inf) or
+ * FEDAVG_ERR_NAN_RESULT (a receiver's result, e.g. 0/0, or the centralized average). */
+int32_t fedavg_pers_check(fedavg_pers* p, void* stream, uint32_t* flags_out);
+int32_t fedavg_pers_prof_enable(fedavg_pers* p, int32_t enable);
+int32_t fedavg_pers_prof_collect(fedavg_pers* p, double* total_ms, int32_t* launches);
+/* fp64 VALU ceiling probe (independent v_fma_f64 chains): measured TFLOP/s */
+int32_t fedavg_fp64_probe(int64_t waves, int32_t iters, double* tflops_out, void* stream);
 
 #ifdef __cplusplus
 }

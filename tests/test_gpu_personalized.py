@@ -1,0 +1,161 @@
+"""HIP PersonalizedFedAVG vs the reference (golden fixtures) and vs the oracle, on the MI355X.
+
+Tolerance: none — every receiver's model and the centralized model are BIT-IDENTICAL to the
+reference's float64 results (asserted with `bits_equal`); float32 outputs equal the reference
+result cast to float32.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_learning_simulation_lib_amd import (
+    MultipleWorkerMessage,
+    NaNAggregationError,
+    ParameterMessage,
+    PersonalizedFedAVGAlgorithm,
+)
+from oracle.fedavg_oracle import OracleMessage
+from oracle.personalized_oracle import OraclePersonalizedFedAvg
+from tests.golden_io import bits_equal, load_personalized
+
+pytestmark = pytest.mark.gpu
+CASES = load_personalized()
+
+
+def run_hip(case, device, from_host=False):
+    algo = PersonalizedFedAVGAlgorithm(device=device)
+    algo.set_worker_weights({j: dict(v) for j, v in case.worker_weights.items()})
+    for a in case.arrivals:
+        msg = None
+        if a.arrays is not None:
+            msg = ParameterMessage(parameter=case.torch_params(a, "cpu" if from_host else device),
+                                   other_data=dict(a.other_data))
+        algo.process_worker_data(a.worker_id, msg)
+    return algo.aggregate_worker_data()
+
+
+@pytest.mark.parametrize("from_host", [False, True])
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_personalized_matches_reference(hip_device, name, from_host):
+    case = CASES[name]
+    if case.error is not None:
+        exc = {"AssertionError": AssertionError, "RuntimeError": RuntimeError}[case.error]
+        with pytest.raises(exc):
+            run_hip(case, hip_device, from_host)
+        return
+    res = run_hip(case, hip_device, from_host)
+    assert isinstance(res, MultipleWorkerMessage)
+    assert list(res.worker_data) == [r["worker_id"] for r in case.meta["receivers"]]
+    for r in case.meta["receivers"]:
+        got = res.worker_data[r["worker_id"]]
+        assert list(got.parameter) == r["keys"]
+        for k, want in case.expected[r["worker_id"]].items():
+            assert bits_equal(got.parameter[k].cpu().numpy(), want), f"{name}/{r['worker_id']}/{k}"
+        assert got.other_data == r["other_data"]
+        assert (got.in_round, got.end_training) == (r["in_round"], r["end_training"])
+    central = res.other_data["centralized_parameter"]
+    assert list(central) == case.meta["central_keys"]
+    for k, want in case.central.items():
+        assert bits_equal(central[k].cpu().numpy(), want), f"{name}/central/{k}"
+
+
+def _random_round(n, receivers, shapes, seed, dtype=torch.float32, weight_kind="float", missing=None):
+    g = torch.Generator().manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    clients = []
+    for k in range(n):
+        p = {name: torch.randn(s, generator=g).to(dtype) for name, s in shapes.items()}
+        if missing and k in missing:
+            del p[missing[k]]
+        clients.append(p)
+    ww = {}
+    for j in receivers:
+        if weight_kind == "int":
+            ww[j] = {i: int(rng.integers(1, 5000)) for i in range(n) if i != j}
+        else:
+            ww[j] = {i: float(rng.uniform(0.01, 3.0)) for i in range(n) if i != j}
+    return clients, ww
+
+
+def _oracle(clients, ww, dtype_name=None):
+    o = OraclePersonalizedFedAvg()
+    o.set_worker_weights({j: dict(v) for j, v in ww.items()})
+    for k, p in enumerate(clients):
+        arrs = {}
+        for name, t in p.items():
+            arrs[name] = t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
+        o.process_worker_data(k, OracleMessage(parameter=arrs, dtype=dtype_name))
+    return o.aggregate_worker_data()
+
+
+def _hip(clients, ww, device, result_dtype=torch.float64, unaligned=False):
+    algo = PersonalizedFedAVGAlgorithm(device=device, result_dtype=result_dtype)
+    algo.set_worker_weights({j: dict(v) for j, v in ww.items()})
+    for k, p in enumerate(clients):
+        dp = {}
+        for name, t in p.items():
+            if unaligned:  # a view one element into a bigger buffer: the guarded-load path
+                buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=device)
+                buf[1:].copy_(t.reshape(-1))
+                dp[name] = buf[1:].view(t.shape)
+            else:
+                dp[name] = t.to(device)
+        algo.process_worker_data(k, ParameterMessage(parameter=dp))
+    return algo.aggregate_worker_data()
+
+
+def _assert_same(res, want, result_dtype=torch.float64):
+    for j, r in want.worker_data.items():
+        for k, v in r.parameter.items():
+            got = res.worker_data[j].parameter[k].cpu()
+            if result_dtype == torch.float64:
+                assert bits_equal(got.numpy(), v), f"receiver {j} / {k}"
+            else:
+                assert torch.equal(got, torch.from_numpy(np.asarray(v)).to(torch.float32)), f"receiver {j} / {k}"
+    for k, v in want.centralized_parameter.items():
+        assert bits_equal(res.other_data["centralized_parameter"][k].cpu().numpy(), v), f"central / {k}"
+
+
+SHAPES = {"conv": (32, 16, 3, 3), "bn": (32,), "fc": (10, 300), "odd": (1001,), "s": ()}
+
+
+@pytest.mark.parametrize("weight_kind", ["float", "int"])
+def test_random_round_matches_oracle(hip_device, weight_kind):
+    clients, ww = _random_round(24, range(24), SHAPES, 101, weight_kind=weight_kind)
+    _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))
+
+
+def test_two_receiver_groups_carry_the_central_chain(hip_device):
+    # 130 receivers > 120 per launch: the second launch continues the centralized chain
+    clients, ww = _random_round(130, range(130), {"a": (257,), "b": (3, 5)}, 102)
+    _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))
+
+
+def test_unaligned_views_and_float32_results(hip_device):
+    clients, ww = _random_round(9, range(9), SHAPES, 103)
+    want = _oracle(clients, ww)
+    _assert_same(_hip(clients, ww, hip_device, unaligned=True), want)
+    _assert_same(_hip(clients, ww, hip_device, result_dtype=torch.float32), want, torch.float32)
+
+
+def test_missing_tensor_in_a_later_update(hip_device):
+    clients, ww = _random_round(7, range(7), SHAPES, 104, missing={3: "fc", 5: "bn"})
+    _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float64])
+def test_other_input_dtypes(hip_device, dtype):
+    clients, ww = _random_round(11, [0, 3, 5, 7, 10], SHAPES, 105, dtype=dtype)
+    name = {torch.bfloat16: "bfloat16"}.get(dtype)
+    _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww, name))
+
+
+def test_nan_input_names_the_worker(hip_device):
+    clients, ww = _random_round(5, range(5), {"a": (100,)}, 106)
+    clients[3]["a"][7] = float("nan")
+    with pytest.raises(NaNAggregationError) as ei:
+        _hip(clients, ww, hip_device)
+    assert ei.value.stage == "input" and ei.value.bad_clients == [3]

@@ -8,6 +8,7 @@ entry point raises. The symbols bound here are exactly the ones the header decla
 from __future__ import annotations
 
 import ctypes
+import os
 from ctypes import POINTER, c_double, c_int32, c_int64, c_uint32, c_void_p
 from typing import Any
 
@@ -126,7 +127,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    lib_path = path or str(LIB_PATH)
+    # FEDAVG_HIP_LIB: load a tuning build instead of the in-tree library (scripts/ A/B runs)
+    lib_path = path or os.environ.get("FEDAVG_HIP_LIB") or str(LIB_PATH)
     try:
         lib = ctypes.CDLL(lib_path)
     except OSError as e:

@@ -1151,7 +1151,7 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
     off += static_cast<int64_t>(align_up(static_cast<size_t>(seg_numel[t]), 2));
   }
   c->acc_numel = off;
-  c->wsum.assign(num_segments, 0.0);
+  c->wsum.assign(num_segments, -0.0);  // additive identity: the first weight is taken as is
   c->valid.assign(num_segments, 0);
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);
@@ -1260,7 +1260,7 @@ int32_t fedavg_set_fused_fold(fedavg_ctx* c, int32_t enable) {
 int32_t fedavg_reset(fedavg_ctx* c, void* stream) {
   FEDAVG_RET(check_ctx(c));
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
-  std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
+  std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
   FEDAVG_HIP_TRY(hipMemsetAsync(c->d_flag, 0, sizeof(uint32_t) * 4, static_cast<hipStream_t>(stream)));
   return FEDAVG_OK;
@@ -1326,7 +1326,7 @@ int32_t fedavg_aggregate(fedavg_ctx* c, const void* const* client_ptrs, int32_t 
   FEDAVG_RET(launch_main(c, s, st, K > 0 ? in_dtype : FEDAVG_F32, ok, split, 0, 0,
                          static_cast<int32_t>(c->tiles1.size())));
   // _aggregate_parameter resets the accumulator (fed_avg_algorithm.py:90,98)
-  std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
+  std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
   return FEDAVG_OK;
 }
@@ -1385,7 +1385,7 @@ int32_t fedavg_aggregate_delta(fedavg_ctx* c, const void* const* client_ptrs, in
                           c->valid.data(), st, base_ptrs));
   FEDAVG_RET(launch_main(c, s, st, K > 0 ? in_dtype : FEDAVG_F32, ok, 1, 0, 0,
                          static_cast<int32_t>(c->tiles1.size())));
-  std::fill(c->wsum.begin(), c->wsum.end(), 0.0);
+  std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
   return FEDAVG_OK;
 }
@@ -1575,7 +1575,7 @@ int32_t fedavg_plan_create(fedavg_ctx* c, const void* const* client_ptrs, int32_
   const int ok = out_kind_of(out_dtype);
   if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
   if (!out_ptrs) return fail(FEDAVG_ERR_INVALID, "null out table");
-  std::vector<double> wtot(c->T, 0.0);
+  std::vector<double> wtot(c->T, -0.0);
   std::vector<int32_t> has(c->T, 0);
   for (int k = 0; k < K; ++k)
     for (int t = 0; t < c->T; ++t)

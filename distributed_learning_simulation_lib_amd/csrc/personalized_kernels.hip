@@ -15,19 +15,20 @@
 // bit-identical, which no MFMA instruction computes (its internal reduction order and
 // rounding are not the reference's). So the contraction runs on the fp64 VALU, register-
 // blocked:
-//   * a workgroup owns a 128-element chunk of one segment (64 lanes x 2 elements) and up to
-//     64 receivers: wave w holds the fp64 accumulators of receivers [16w, 16w+16) for the
-//     lane's 2 elements (64 VGPRs);
-//   * clients stream in arrival order; each client's chunk is loaded once per wave (the four
-//     waves of a workgroup read the same 512 B, served by the CU's L1 / the XCD's L2, so HBM
-//     sees every client byte once per receiver group) and folded into 16 receivers x 2
-//     elements: 32 fp64 (mul, add) pairs per 8-byte load — VALU-bound, ~4 flop/byte;
-//   * the receiver's own update is excluded (:31-32) with a per-(client, wave) fold mask: the
-//     common case (no receiver of this wave excludes the client) is branch-free;
-//   * epilogue: divide by the receiver's per-segment total, store out_j, and fold the
-//     centralized average across the waves in receiver order through LDS (one barrier per
-//     wave); receivers beyond 64 run as further launches that carry the centralized chain
-//     in an fp64 scratch buffer.
+//   * a workgroup owns a 256-element chunk of one segment (64 lanes x 4 elements) and up to
+//     128 receivers: wave w holds the fp64 accumulators of receivers [16w, 16w+16) for the
+//     lane's 4 elements (128 VGPRs);
+//   * clients stream in arrival order, the next client group's 16-B loads in flight while a
+//     group folds; the waves of a workgroup read the same 1 KiB per client (CU L1 / XCD L2:
+//     HBM sees every client byte once per launch); weights are wave-uniform SGPR operands;
+//     every 16-B load feeds 16 receivers x 4 elements = 64 fp64 folds — VALU-bound;
+//   * the pairs the reference skips (a receiver's own update :31-32, absent tensors, padding)
+//     fold with weight 0, which is exact except for ±0 / NaN sums — those elements alone are
+//     re-folded with the pairs skipped (the loop stays branch-free);
+//   * epilogue: divide by the receiver's per-segment total (IEEE division), store out_j, and
+//     fold the centralized average across the waves in receiver order through LDS (one
+//     barrier per wave); receivers beyond 128 run as further launches that carry the
+//     centralized chain in an fp64 scratch buffer.
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
@@ -60,12 +61,21 @@ int32_t pfail(int32_t code, const std::string& msg) { return fedavg_internal_fai
     if (r_ != FEDAVG_OK) return r_; \
   } while (0)
 
-constexpr int kVE = 2;                 // elements per lane
+#ifndef PERS_VE
+#define PERS_VE 4
+#endif
+constexpr int kVE = PERS_VE;           // elements per lane
 constexpr int kChunk = 64 * kVE;       // elements per workgroup
 constexpr int kJB = 16;                // receivers per wave
 constexpr int kMaxWaves = 8;           // waves per workgroup
 constexpr int kGroup = kMaxWaves * kJB;  // receivers per launch (128)
-constexpr int kU = 4;                  // clients loaded ahead per lane
+#ifndef PERS_U  // 2 keeps every dtype/fold at <= 168 VGPRs = 3 waves per SIMD (measured best)
+#define PERS_U 2
+#endif
+constexpr int kU = PERS_U;             // clients loaded ahead per lane
+#ifndef PERS_LDS_PAD  // tuning: LDS bytes reserved per workgroup (caps resident workgroups per CU)
+#define PERS_LDS_PAD 0
+#endif
 
 struct PChunk {
   int32_t seg;
@@ -125,55 +135,76 @@ __device__ __forceinline__ double h2d(uint32_t h) {
 }
 __device__ __forceinline__ double b2d(uint32_t b) { return static_cast<double>(__uint_as_float(b << 16)); }
 
-// Raw (undecoded) 2-element slice of one client chunk for one lane: loaded one client group
+// Raw (undecoded) kVE-element slice of one client chunk for one lane: loaded one client group
 // ahead of the fold (software pipelining), expanded to doubles when folded.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <typename T>
 struct Raw;
 template <>
 struct Raw<float> {
-  using type = f32x2;
+  using type = f32x4;
   static constexpr int kSize = 4;
-  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const f32x2>)((gp<const float>)b + e)); }
+  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const f32x4>)((gp<const float>)b + e)); }
   __device__ __forceinline__ static type guarded(uint64_t b, int e, int count) {
     type v;
     v.x = (e < count) ? ((gp<const float>)b)[e] : 0.f;
     v.y = (e + 1 < count) ? ((gp<const float>)b)[e + 1] : 0.f;
+    v.z = (e + 2 < count) ? ((gp<const float>)b)[e + 2] : 0.f;
+    v.w = (e + 3 < count) ? ((gp<const float>)b)[e + 3] : 0.f;
     return v;
   }
-  __device__ __forceinline__ static void expand(type v, double& x0, double& x1) {
-    x0 = v.x;
-    x1 = v.y;
+  __device__ __forceinline__ static void expand(type v, double* x) {
+    x[0] = v.x;
+    x[1] = v.y;
+    x[2] = v.z;
+    x[3] = v.w;
   }
+};
+struct f64x2x2 {
+  f64x2 lo, hi;
 };
 template <>
 struct Raw<double> {
-  using type = f64x2;
+  using type = f64x2x2;
   static constexpr int kSize = 8;
-  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const f64x2>)((gp<const double>)b + e)); }
+  __device__ __forceinline__ static type full(uint64_t b, int e) {
+    const gp<const f64x2> p = (gp<const f64x2>)((gp<const double>)b + e);
+    return type{p[0], p[1]};
+  }
   __device__ __forceinline__ static type guarded(uint64_t b, int e, int count) {
+    const gp<const double> p = (gp<const double>)b;
     type v;
-    v.x = (e < count) ? ((gp<const double>)b)[e] : 0.0;
-    v.y = (e + 1 < count) ? ((gp<const double>)b)[e + 1] : 0.0;
+    v.lo.x = (e < count) ? p[e] : 0.0;
+    v.lo.y = (e + 1 < count) ? p[e + 1] : 0.0;
+    v.hi.x = (e + 2 < count) ? p[e + 2] : 0.0;
+    v.hi.y = (e + 3 < count) ? p[e + 3] : 0.0;
     return v;
   }
-  __device__ __forceinline__ static void expand(type v, double& x0, double& x1) {
-    x0 = v.x;
-    x1 = v.y;
+  __device__ __forceinline__ static void expand(type v, double* x) {
+    x[0] = v.lo.x;
+    x[1] = v.lo.y;
+    x[2] = v.hi.x;
+    x[3] = v.hi.y;
   }
 };
 template <typename H>
-struct Raw16 {  // 2-byte inputs: both elements in one dword
-  using type = uint32_t;
+struct Raw16 {  // 2-byte inputs: two elements per dword
+  using type = u32x2;
   static constexpr int kSize = 2;
-  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const uint32_t>)((gp<const uint16_t>)b + e)); }
+  __device__ __forceinline__ static type full(uint64_t b, int e) { return *((gp<const u32x2>)((gp<const uint16_t>)b + e)); }
   __device__ __forceinline__ static type guarded(uint64_t b, int e, int count) {
-    const uint32_t lo = (e < count) ? ((gp<const uint16_t>)b)[e] : 0u;
-    const uint32_t hi = (e + 1 < count) ? ((gp<const uint16_t>)b)[e + 1] : 0u;
-    return lo | (hi << 16);
+    const gp<const uint16_t> p = (gp<const uint16_t>)b;
+    uint32_t h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = (e + i < count) ? p[e + i] : 0u;
+    return u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
   }
-  __device__ __forceinline__ static void expand(type v, double& x0, double& x1) {
-    x0 = H::cvt(v & 0xffffu);
-    x1 = H::cvt(v >> 16);
+  __device__ __forceinline__ static void expand(type v, double* x) {
+    x[0] = H::cvt(v.x & 0xffffu);
+    x[1] = H::cvt(v.x >> 16);
+    x[2] = H::cvt(v.y & 0xffffu);
+    x[3] = H::cvt(v.y >> 16);
   }
 };
 struct HalfCvt {
@@ -186,6 +217,7 @@ template <>
 struct Raw<__half> : Raw16<HalfCvt> {};
 template <>
 struct Raw<bf16_t> : Raw16<Bf16Cvt> {};
+static_assert(kVE == 4, "the Raw loaders move 4 elements per lane");
 
 enum PFold : int { PF_MULADD = 0, PF_FMA = 1 };
 
@@ -218,13 +250,41 @@ __device__ __forceinline__ typename Raw<T>::type load_raw(uint64_t b, int e, int
   }
 }
 
+__device__ __forceinline__ bool zero_or_nan(double v) { return v == 0.0 || v != v; }
+
+// Store one receiver's kVE results of the lane (non-temporal vector stores on whole chunks).
+template <bool FULL>
+__device__ __forceinline__ void store_result(uint64_t op, int64_t start, int e, int count, bool f32, const double* r) {
+  if (f32) {
+    gp<float> o = (gp<float>)(reinterpret_cast<void*>(op)) + start + e;
+    if (FULL) {
+      __builtin_nontemporal_store(f32x4{static_cast<float>(r[0]), static_cast<float>(r[1]),
+                                        static_cast<float>(r[2]), static_cast<float>(r[3])}, (gp<f32x4>)o);
+    } else {
+#pragma unroll
+      for (int v = 0; v < kVE; ++v)
+        if (e + v < count) o[v] = static_cast<float>(r[v]);
+    }
+  } else {
+    gp<double> o = (gp<double>)(reinterpret_cast<void*>(op)) + start + e;
+    if (FULL) {
+      __builtin_nontemporal_store(f64x2{r[0], r[1]}, (gp<f64x2>)o);
+      __builtin_nontemporal_store(f64x2{r[2], r[3]}, (gp<f64x2>)(o + 2));
+    } else {
+#pragma unroll
+      for (int v = 0; v < kVE; ++v)
+        if (e + v < count) o[v] = r[v];
+    }
+  }
+}
+
 // The main loop. Every receiver of the wave folds every client of the (padded) arrival list:
 // the pairs the reference skips — a receiver's own update (:31-32), an absent tensor, padding —
 // carry weight 0. Folding x*0 into acc is exact (acc + ±0 == acc) except when acc is -0.0 and
 // the product +0.0 (the sum becomes +0.0) or x is inf/NaN (the product is NaN); both leave a
 // receiver's final sum at ±0 or NaN, so those — and only those — elements are re-folded at the
 // end with the skipped pairs really skipped (refold below). The loop itself has no branches
-// and no per-receiver tests: 16 receivers x 2 elements fold per 8-byte load, with the next
+// and no per-receiver tests: 16 receivers x 4 elements fold per 16-byte load, with the next
 // client group's loads in flight.
 template <typename T, int FOLD, bool FULL>
 __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, int seg, int count, int64_t start,
@@ -238,11 +298,13 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
   const kp<uint64_t> ptrs = (kp<uint64_t>)(a.cptrs) + static_cast<int64_t>(seg) * a.Npad;
   const kp<double> wt = (kp<double>)(a.w) + j0;
 
-  // fp64 accumulators of the wave's 16 receivers for the lane's two elements, started at the
+  // fp64 accumulators of the wave's 16 receivers for the lane's kVE elements, started at the
   // IEEE additive identity (-0.0 + p == p: the first fold equals the reference's assignment)
-  double acc0[kJB], acc1[kJB];
+  double acc[kVE][kJB];
 #pragma unroll
-  for (int j = 0; j < kJB; ++j) acc0[j] = acc1[j] = -0.0;
+  for (int v = 0; v < kVE; ++v)
+#pragma unroll
+    for (int j = 0; j < kJB; ++j) acc[v][j] = -0.0;
 
   RT nxt[kU];
 #pragma unroll
@@ -259,84 +321,70 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      double x0, x1;
-      R::expand(cur[u], x0, x1);
+      double x[kVE];
+      R::expand(cur[u], x);
       const kp<double> wk = wt + static_cast<int64_t>(k + u) * a.wstride;
 #pragma unroll
       for (int j = 0; j < kJB; ++j) {
         const double wj = wk[j];
-        acc0[j] = pfold<FOLD>(acc0[j], x0, wj);
-        acc1[j] = pfold<FOLD>(acc1[j], x1, wj);
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wj);
       }
     }
   }
 
-  const bool in0 = e < count, in1 = e + 1 < count;
+  bool in[kVE];
+#pragma unroll
+  for (int v = 0; v < kVE; ++v) in[v] = e + v < count;
   // refold (rare): elements whose sum is ±0 or NaN are recomputed with the skipped pairs
-  // skipped, giving the reference's exact sign of zero / its NaN-or-not verdict
-  bool fix = false;
+  // skipped, giving the reference's exact sign of zero / its NaN-or-not verdict. One receiver
+  // at a time, so the rare path adds no register pressure to the main loop.
+  const kp<int32_t> exm = (kp<int32_t>)(a.exmask);
 #pragma unroll
-  for (int j = 0; j < kJB; ++j)
-    fix |= (in0 && (acc0[j] == 0.0 || acc0[j] != acc0[j])) || (in1 && (acc1[j] == 0.0 || acc1[j] != acc1[j]));
-  if (__ballot(fix) != 0ull) {
-    double b0[kJB], b1[kJB];
+  for (int j = 0; j < kJB; ++j) {
+    bool f[kVE], any = false;
 #pragma unroll
-    for (int j = 0; j < kJB; ++j) b0[j] = b1[j] = -0.0;
-    const kp<int32_t> exm = (kp<int32_t>)(a.exmask);
+    for (int v = 0; v < kVE; ++v) {
+      f[v] = in[v] && zero_or_nan(acc[v][j]);
+      any |= f[v];
+    }
+    if (__ballot(any) == 0ull) continue;
+    double b[kVE];
+#pragma unroll
+    for (int v = 0; v < kVE; ++v) b[v] = -0.0;
     for (int k = 0; k < a.N; ++k) {
       const uint64_t p = ptrs[k];
       if (!p) continue;  // absent tensor: nobody folds it
-      const uint32_t em = static_cast<uint32_t>(exm[static_cast<int64_t>(k) * a.waves + wave]);
-      double x0, x1;
-      R::expand(load_raw<T, FULL>(p + sb, e, count), x0, x1);
-      const kp<double> wk = wt + static_cast<int64_t>(k) * a.wstride;
+      if ((static_cast<uint32_t>(exm[static_cast<int64_t>(k) * a.waves + wave]) >> j) & 1u) continue;  // own update
+      double x[kVE];
+      R::expand(load_raw<T, FULL>(p + sb, e, count), x);
+      const double wj = wt[static_cast<int64_t>(k) * a.wstride + j];
 #pragma unroll
-      for (int j = 0; j < kJB; ++j) {
-        if ((em >> j) & 1u) continue;  // receiver j's own update
-        b0[j] = pfold<FOLD>(b0[j], x0, wk[j]);
-        b1[j] = pfold<FOLD>(b1[j], x1, wk[j]);
-      }
+      for (int v = 0; v < kVE; ++v) b[v] = pfold<FOLD>(b[v], x[v], wj);
     }
 #pragma unroll
-    for (int j = 0; j < kJB; ++j) {
-      if (acc0[j] == 0.0 || acc0[j] != acc0[j]) acc0[j] = b0[j];
-      if (acc1[j] == 0.0 || acc1[j] != acc1[j]) acc1[j] = b1[j];
-    }
+    for (int v = 0; v < kVE; ++v)
+      if (f[v]) acc[v][j] = b[v];
   }
 
-  // epilogue: out_j = acc_j / W_j with the fused NaN assertions (fed_avg_algorithm.py:92-97)
+  // epilogue: out_j = acc_j / W_j with the fused NaN assertions (fed_avg_algorithm.py:92-97);
+  // the quotients stay in acc for the centralized average
   bool bad_acc = false, bad_res = false;
   const kp<double> wtot = (kp<double>)(a.wtot);
   const kp<uint64_t> outs = (kp<uint64_t>)(a.outs);
-  double r0[kJB], r1[kJB];
 #pragma unroll
   for (int j = 0; j < kJB; ++j) {
-    r0[j] = acc0[j];
-    r1[j] = acc1[j];
     if (j0 + j >= a.M) continue;  // (continue, not break: keeps the loop fully unrolled)
     const double W = wtot[static_cast<int64_t>(j0 + j) * a.T + seg];
-    bad_acc |= (in0 && r0[j] != r0[j]) || (in1 && r1[j] != r1[j]);
-    r0[j] = r0[j] / W;
-    r1[j] = r1[j] / W;
-    bad_res |= (in0 && r0[j] != r0[j]) || (in1 && r1[j] != r1[j]);
-    const uint64_t op = outs[static_cast<int64_t>(j0 + j) * a.T + seg];
-    if (a.out_f32) {
-      gp<float> o = (gp<float>)(reinterpret_cast<void*>(op)) + start + e;
-      if (FULL) {
-        __builtin_nontemporal_store(f32x2{static_cast<float>(r0[j]), static_cast<float>(r1[j])}, (gp<f32x2>)o);
-      } else {
-        if (in0) o[0] = static_cast<float>(r0[j]);
-        if (in1) o[1] = static_cast<float>(r1[j]);
-      }
-    } else {
-      gp<double> o = (gp<double>)(reinterpret_cast<void*>(op)) + start + e;
-      if (FULL) {
-        __builtin_nontemporal_store(f64x2{r0[j], r1[j]}, (gp<f64x2>)o);
-      } else {
-        if (in0) o[0] = r0[j];
-        if (in1) o[1] = r1[j];
-      }
+    double r[kVE];
+#pragma unroll
+    for (int v = 0; v < kVE; ++v) {
+      bad_acc |= in[v] && acc[v][j] != acc[v][j];
+      acc[v][j] = acc[v][j] / W;
+      bad_res |= in[v] && acc[v][j] != acc[v][j];
+      r[v] = acc[v][j];
     }
+    store_result<FULL>(outs[static_cast<int64_t>(j0 + j) * a.T + seg], start, e, count, a.out_f32, r);
   }
   if (__ballot(bad_acc) != 0ull && lane == 0) pflag(a.flag, 0);
   if (__ballot(bad_res) != 0ull && lane == 0) pflag(a.flag, 1);
@@ -347,43 +395,39 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
   const int64_t coff = a.seg_off[seg] + start + e;
   for (int s = 0; s < a.waves; ++s) {
     if (wave == s) {
-      double c0, c1;
-      if (s > 0) {
-        c0 = chain[lane * kVE];
-        c1 = chain[lane * kVE + 1];
-      } else if (a.central_in) {
-        c0 = in0 ? a.carry[coff] : -0.0;
-        c1 = in1 ? a.carry[coff + 1] : -0.0;
-      } else {
-        c0 = c1 = -0.0;
+      double c[kVE];
+#pragma unroll
+      for (int v = 0; v < kVE; ++v) {
+        if (s > 0) {
+          c[v] = chain[lane * kVE + v];
+        } else if (a.central_in) {
+          c[v] = in[v] ? a.carry[coff + v] : -0.0;
+        } else {
+          c[v] = -0.0;
+        }
       }
 #pragma unroll
       for (int j = 0; j < kJB; ++j) {
         if (j0 + j >= a.M) continue;
-        const double d0 = r0[j] * a.cw;  // v.to(float64) * weight   (:65-68)
-        const double d1 = r1[j] * a.cw;
-        c0 = c0 + d0;                    // avg_data[k] += d[k]       (:72)
-        c1 = c1 + d1;
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) {
+          const double d = acc[v][j] * a.cw;  // v.to(float64) * weight   (:65-68)
+          c[v] = c[v] + d;                    // avg_data[k] += d[k]       (:72)
+        }
       }
       if (s + 1 < a.waves) {
-        chain[lane * kVE] = c0;
-        chain[lane * kVE + 1] = c1;
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) chain[lane * kVE + v] = c[v];
       } else if (a.central_mode == CENTRAL_CARRY_OUT) {
-        if (in0) a.carry[coff] = c0;
-        if (in1) a.carry[coff + 1] = c1;
+#pragma unroll
+        for (int v = 0; v < kVE; ++v)
+          if (in[v]) a.carry[coff + v] = c[v];
       } else {
-        const bool bad = (in0 && c0 != c0) || (in1 && c1 != c1);  // (:73-74)
+        bool bad = false;  // (:73-74)
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) bad |= in[v] && c[v] != c[v];
         if (__ballot(bad) != 0ull && lane == 0) pflag(a.flag, 2);
-        const uint64_t op = ((kp<uint64_t>)(a.central))[seg];
-        if (a.central_f32) {
-          gp<float> o = (gp<float>)(reinterpret_cast<void*>(op)) + start + e;
-          if (in0) o[0] = static_cast<float>(c0);
-          if (in1) o[1] = static_cast<float>(c1);
-        } else {
-          gp<double> o = (gp<double>)(reinterpret_cast<void*>(op)) + start + e;
-          if (in0) o[0] = c0;
-          if (in1) o[1] = c1;
-        }
+        store_result<false>(((kp<uint64_t>)(a.central))[seg], start, e, count, a.central_f32, c);
       }
     }
     if (s + 1 < a.waves) __syncthreads();
@@ -392,9 +436,10 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 
 template <typename T, int FOLD>
 __global__ __launch_bounds__(64 * kMaxWaves) void personalized_kernel(PArgs a) {
-  __shared__ double chain[64 * kVE];
+  __shared__ double chain[64 * kVE + PERS_LDS_PAD / 8];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
+  if (PERS_LDS_PAD > 0 && threadIdx.x == 4096) chain[64 * kVE] = 0.0;  // keeps the pad allocated
   const kp<int32_t> cd = (kp<int32_t>)(a.chunks + blockIdx.x);
   const int seg = cd[0];
   const int count = cd[1];
@@ -601,10 +646,10 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
     for (int i = 0; i < j; ++i)
       if (receiver_ids[i] == receiver_ids[j]) return pfail(FEDAVG_ERR_INVALID, "duplicate receiver id");
   bool aligned = true;
-  const size_t in_align = static_cast<size_t>(elem_size(in_dtype)) * kVE;
+  const size_t in_align = std::min<size_t>(16, static_cast<size_t>(elem_size(in_dtype)) * kVE);
   for (int64_t i = 0; i < static_cast<int64_t>(M) * T; ++i) {
     if (!out_ptrs[i]) return pfail(FEDAVG_ERR_INVALID, "null output pointer");
-    if (reinterpret_cast<uintptr_t>(out_ptrs[i]) % (out_dtype == FEDAVG_F64 ? 16 : 8) != 0) aligned = false;
+    if (reinterpret_cast<uintptr_t>(out_ptrs[i]) % 16 != 0) aligned = false;
   }
   for (int64_t i = 0; i < static_cast<int64_t>(N) * T; ++i)
     if (client_ptrs[i] && reinterpret_cast<uintptr_t>(client_ptrs[i]) % in_align != 0) aligned = false;
@@ -619,10 +664,15 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
   for (int k = 0; k < N; ++k)
     for (int j = 0; j < M; ++j)
       if (receiver_ids[j] == client_ids[k]) excl[k] = j;
-  std::vector<double> wtot(static_cast<size_t>(M) * T, 0.0);
+  // sums start at -0.0, the additive identity: the first weight is taken as is (python `= w`)
+  std::vector<double> wtot(static_cast<size_t>(M) * T, -0.0);
   std::vector<uint8_t> have(static_cast<size_t>(M) * T, 0);
+  bool all_whole = true;  // every client sent every tensor (the server complete()s messages)
+  for (int64_t i = 0; i < static_cast<int64_t>(N) * T && all_whole; ++i) all_whole = client_ptrs[i] != nullptr;
   int max_bits = 0;
   bool tame = true;
+  std::vector<double> run(M, -0.0);  // all_whole: one arrival-order sum per receiver
+  std::vector<uint8_t> any(M, 0);
   for (int k = 0; k < N; ++k) {
     for (int j = 0; j < M; ++j) {
       if (excl[k] == j) continue;
@@ -630,6 +680,11 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
       const int b = weight_bits(w);
       if (b < 0) tame = false;
       max_bits = std::max(max_bits, b);
+      if (all_whole) {
+        run[j] += w;
+        any[j] = 1;
+        continue;
+      }
       for (int t = 0; t < T; ++t) {
         if (!client_ptrs[static_cast<int64_t>(k) * T + t]) continue;
         wtot[static_cast<size_t>(j) * T + t] += w;
@@ -637,6 +692,12 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
       }
     }
   }
+  if (all_whole)
+    for (int j = 0; j < M; ++j)
+      for (int t = 0; t < T; ++t) {
+        wtot[static_cast<size_t>(j) * T + t] = run[j];
+        have[static_cast<size_t>(j) * T + t] = any[j];
+      }
   for (int j = 0; j < M; ++j)
     for (int t = 0; t < T; ++t)
       if (!have[static_cast<size_t>(j) * T + t])

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 from collections.abc import Sequence
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -21,6 +22,21 @@ from .fedavg import ModelLayout, dtype_code, out_code
 _PTR = ctypes.POINTER(ctypes.c_void_p)
 _DBL = ctypes.POINTER(ctypes.c_double)
 _I64 = ctypes.POINTER(ctypes.c_int64)
+
+
+@dataclass(frozen=True)
+class PersonalizedTables:
+    """Validated device pointers of one round's clients and outputs (C-ABI arrays)."""
+
+    num_clients: int
+    num_receivers: int
+    in_dtype: torch.dtype
+    out_dtype: torch.dtype
+    central_dtype: torch.dtype
+    ptrs: np.ndarray
+    optrs: np.ndarray
+    cptrs: np.ndarray | None
+    keep: tuple
 
 
 class PersonalizedContext:
@@ -61,26 +77,19 @@ class PersonalizedContext:
     def set_fused_fold(self, enable: bool) -> None:
         _native.check(self._lib.fedavg_pers_set_fused_fold(self._h, 1 if enable else 0))
 
-    def aggregate(
+    def tables(
         self,
         clients: Sequence[Sequence[torch.Tensor | None]],
         in_dtype: torch.dtype,
-        client_ids: Sequence[int],
-        weights: np.ndarray,
-        receiver_ids: Sequence[int],
         outs: Sequence[Sequence[torch.Tensor]],
         out_dtype: torch.dtype,
         central: Sequence[torch.Tensor] | None = None,
         central_dtype: torch.dtype = torch.float64,
-    ) -> None:
-        """clients[N][T] (None = tensor not sent), weights[M][N] (float64), outs[M][T]."""
+    ) -> PersonalizedTables:
+        """Validate the tensors of a round once (persistent client / output slots reuse it)."""
         T = self.layout.num_segments
-        N, M = len(clients), len(receiver_ids)
-        w = np.ascontiguousarray(weights, dtype=np.float64)
-        if w.shape != (M, N) or len(client_ids) != N or len(outs) != M:
-            raise ValueError("clients, weights, ids and outputs disagree on N / M")
         numels = self.layout.numels
-        ptrs = np.zeros(N * T, dtype=np.uint64)
+        ptrs = np.zeros(len(clients) * T, dtype=np.uint64)
         keep: list[torch.Tensor] = []
         for k, row in enumerate(clients):
             if len(row) != T:
@@ -92,7 +101,7 @@ class PersonalizedContext:
                     raise ValueError("client tensors must be contiguous, on the device, of the input dtype and size")
                 ptrs[k * T + t] = x.data_ptr()
                 keep.append(x)
-        optrs = np.zeros(M * T, dtype=np.uint64)
+        optrs = np.zeros(len(outs) * T, dtype=np.uint64)
         for j, row in enumerate(outs):
             for t, o in enumerate(row):
                 if o.device != self.device or o.dtype != out_dtype or o.numel() != numels[t] or not o.is_contiguous():
@@ -101,22 +110,43 @@ class PersonalizedContext:
                 keep.append(o)
         cptrs = None
         if central is not None:
-            cp = np.zeros(T, dtype=np.uint64)
+            cptrs = np.zeros(T, dtype=np.uint64)
             for t, o in enumerate(central):
                 if o.device != self.device or o.dtype != central_dtype or o.numel() != numels[t] or not o.is_contiguous():
                     raise ValueError("centralized outputs must be contiguous, on the device, of the dtype and size")
-                cp[t] = o.data_ptr()
+                cptrs[t] = o.data_ptr()
                 keep.append(o)
-            cptrs = cp
+        return PersonalizedTables(len(clients), len(outs), in_dtype, out_dtype, central_dtype, ptrs, optrs, cptrs,
+                                  tuple(keep))
+
+    def aggregate(
+        self,
+        clients: Sequence[Sequence[torch.Tensor | None]] | PersonalizedTables,
+        in_dtype: torch.dtype,
+        client_ids: Sequence[int],
+        weights: np.ndarray,
+        receiver_ids: Sequence[int],
+        outs: Sequence[Sequence[torch.Tensor]] | None = None,
+        out_dtype: torch.dtype = torch.float64,
+        central: Sequence[torch.Tensor] | None = None,
+        central_dtype: torch.dtype = torch.float64,
+    ) -> None:
+        """clients[N][T] (None = tensor not sent) or prepared tables, weights[M][N] float64."""
+        tab = clients if isinstance(clients, PersonalizedTables) else \
+            self.tables(clients, in_dtype, outs or (), out_dtype, central, central_dtype)
+        N, M = tab.num_clients, len(receiver_ids)
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        if w.shape != (M, N) or len(client_ids) != N or tab.num_receivers != M:
+            raise ValueError("clients, weights, ids and outputs disagree on N / M")
         cid = np.asarray(client_ids, dtype=np.int64)
         rid = np.asarray(receiver_ids, dtype=np.int64)
-        self._keep = (ptrs, optrs, cptrs, cid, rid, w, keep)
+        self._keep = (tab, cid, rid, w)
         _native.check(
             self._lib.fedavg_pers_aggregate(
-                self._h, ptrs.ctypes.data_as(_PTR), dtype_code(in_dtype), N, cid.ctypes.data_as(_I64),
-                w.ctypes.data_as(_DBL), rid.ctypes.data_as(_I64), M, optrs.ctypes.data_as(_PTR),
-                out_code(out_dtype), None if cptrs is None else cptrs.ctypes.data_as(_PTR),
-                out_code(central_dtype), self.stream,
+                self._h, tab.ptrs.ctypes.data_as(_PTR), dtype_code(tab.in_dtype), N, cid.ctypes.data_as(_I64),
+                w.ctypes.data_as(_DBL), rid.ctypes.data_as(_I64), M, tab.optrs.ctypes.data_as(_PTR),
+                out_code(tab.out_dtype), None if tab.cptrs is None else tab.cptrs.ctypes.data_as(_PTR),
+                out_code(tab.central_dtype), self.stream,
             )
         )
 

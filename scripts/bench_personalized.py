@@ -65,8 +65,10 @@ def main() -> int:
     ctx = PersonalizedContext(layout, device)
     ids = list(range(N))
 
+    tables = ctx.tables(clients, torch.float32, outs, out_dtype, central, torch.float64)  # persistent slots
+
     def step():
-        ctx.aggregate(clients, torch.float32, ids, w, ids, outs, out_dtype, central, torch.float64)
+        ctx.aggregate(tables, torch.float32, ids, w, ids)
 
     for _ in range(args.warmup):
         step()

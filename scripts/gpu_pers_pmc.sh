@@ -1,8 +1,12 @@
 #!/bin/bash
-# PMC pass over the personalized bench: where do the waves' cycles go?
+# PMC pass over the personalized bench (FEDAVG_HIP_LIB may select a tuning build)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pers_pmc
-timeout -s KILL 120 rocprofv3 --kernel-trace --stats --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SMEM SQ_WAVES -d gpurun_out/pers_pmc -o pmc1 -- python scripts/bench_personalized.py --steps 2 --warmup 1 --no-probe ${PERS_ARGS:-} > gpurun_out/pers_pmc/run1.log 2>&1 || { echo "pmc1 failed rc=$?"; tail -20 gpurun_out/pers_pmc/run1.log; exit 1; }
-find gpurun_out/pers_pmc -name "*counter_collection.csv" | head
+rm -f gpurun_out/pers_pmc/*.db
+for w in ${WEIGHTS:-float int}; do
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SMEM SQ_WAVES -d gpurun_out/pers_pmc -o pmc_$w -- python scripts/bench_personalized.py --steps 2 --warmup 1 --no-probe --weights $w > gpurun_out/pers_pmc/run_$w.log 2>&1 || { echo "pmc $w failed rc=$?"; tail -20 gpurun_out/pers_pmc/run_$w.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH -d gpurun_out/pers_pmc -o pmc2_$w -- python scripts/bench_personalized.py --steps 2 --warmup 1 --no-probe --weights $w > gpurun_out/pers_pmc/run2_$w.log 2>&1 || { echo "pmc2 $w failed rc=$?"; tail -20 gpurun_out/pers_pmc/run2_$w.log; exit 1; }
+done
+ls gpurun_out/pers_pmc

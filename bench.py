@@ -209,6 +209,140 @@ def cpu_baseline(layout: ModelLayout, budget_s: float = 12.0, sample_clients: in
     }
 
 
+def cpu_baseline_personalized(layout: ModelLayout, budget_s: float = 12.0, workers: int = 5) -> dict:
+    """The reference's PersonalizedFedAVG CPU op sequence on a bounded sample (rank 0, N=1)."""
+    sys.path.insert(0, str(REPO))
+    from oracle.ref_torch_cpu import RefOpsPersonalized
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(1234)
+    clients = [
+        {n: torch.randn(s, generator=g, dtype=torch.float32) for n, s in zip(layout.names, layout.shapes)}
+        for _ in range(workers)
+    ]
+    rng = np.random.default_rng(99)
+    ww = {j: {i: float(rng.uniform(0.01, 3.0)) for i in range(workers) if i != j} for j in range(workers)}
+    nbytes = workers * layout.total_numel * 4 + (workers + 1) * layout.total_numel * 8
+    times = []
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < budget_s and len(times) < 100:
+        algo = RefOpsPersonalized(ww)
+        t0 = time.perf_counter()
+        for i, c in enumerate(clients):
+            algo.add(i, c)
+        algo.finish()
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {
+        "value": round(nbytes / best / 1e9, 3),
+        "unit": "GB/s",
+        "folds_per_s": round(workers * (workers - 1) * layout.total_numel / best, 1),
+        "cores": threads,
+        "kind": "port",
+        "sample": (
+            f"{workers} workers x {workers} receivers x ResNet-18 layout fp32, reference op sequence "
+            "(deepcopy per receiver, isnan, to(f64)*w, +=, /W, isnan; centralized weighted_avg) in torch CPU, "
+            f"best of {len(times)} runs over {time.perf_counter() - t_start:.1f} s"
+        ),
+    }
+
+
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec, vector fp64 (an FMA counts 2 flops)
+
+
+def main_personalized(args: argparse.Namespace) -> int:
+    """--workload personalized: one round of PersonalizedFedAVG (personalized_aggregation_algorithm.py),
+    every worker a receiver (M = N = --clients-per-gpu), device-resident clients, one GPU."""
+    from distributed_learning_simulation_lib_amd.personalized import PersonalizedContext, fp64_probe
+
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(device)
+    layout = LAYOUTS[args.layout]()
+    P, N = layout.total_numel, args.clients_per_gpu
+    M = N
+    in_dtype = getattr(torch, args.in_dtype)
+    out_dtype = torch.float64  # the reference's per-receiver models are float64
+    _, views = make_clients(layout, 0, N, device, in_dtype)
+    rng = np.random.default_rng(99)
+    if args.pers_weights == "int":
+        w = rng.integers(100, 5001, size=(M, N)).astype(np.float64)
+    else:
+        w = rng.uniform(0.01, 3.0, size=(M, N))
+    ooffs, opad = layout.padded_offsets(8)
+    out_bufs = [torch.empty(opad, dtype=out_dtype, device=device) for _ in range(M)]
+    outs = [[b[o : o + n] for o, n in zip(ooffs, layout.numels)] for b in out_bufs]
+    cbuf = torch.empty(opad, dtype=torch.float64, device=device)
+    central = [cbuf[o : o + n] for o, n in zip(ooffs, layout.numels)]
+    ctx = PersonalizedContext(layout, device)
+    tables = ctx.tables(views, in_dtype, outs, out_dtype, central, torch.float64)
+    ids = list(range(N))
+
+    def step() -> None:
+        ctx.aggregate(tables, in_dtype, ids, w, ids)
+        if ctx.check():  # the reference's assertions: the round ends on the host
+            raise AssertionError("NaN in a personalized aggregate")
+
+    for _ in range(args.warmup):
+        step()
+    ctx.prof_enable(True)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = ctx.prof_collect()
+    step_s = elapsed / args.steps
+    kstep_s = kernel_ms * 1e-3 / args.steps
+    in_bytes = torch.empty((), dtype=in_dtype).element_size()
+    job_bytes = N * P * in_bytes + M * P * 8 + P * 8
+    folds = M * (N - 1) * P
+    fused = args.pers_weights == "int"  # integer weights: every product exact -> one v_fma_f64 per fold
+    lane_ops = folds * (1 if fused else 2) + 2 * M * P
+    probe = None if args.no_probe else {"fp64_fma_TFLOPs": round(fp64_probe(device), 2), **hbm_probes(device)}
+    cpu = None
+    if not args.no_cpu_baseline:
+        del views, tables
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline_personalized(layout)
+    short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    line = {
+        "metric": "PersonalizedFedAVG round, aggregated GB/s (device-resident)",
+        "value": round(job_bytes / step_s / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "replicas only",
+        "vs_baseline": None,
+        "folds_per_s": round(folds / step_s, 1),  # (receiver, client, element) folds: the unit of work
+        "dtype": "f64",
+        "data": f"synthetic: client params ~ N(0,1), {args.pers_weights} weights (M x N)",
+        "config": {"workload": f"personalized_fedavg_{args.layout}_{short}_{N}x{M}", "workers": N, "receivers": M,
+                   "params_per_client": P, "tensors_per_client": layout.num_segments, "in_dtype": args.in_dtype,
+                   "out_dtype": "float64", "fold": "fma (exact products)" if fused else "mul + add (rounded separately)"},
+        "roofline": {
+            "bound": "valu_fp64",
+            "achieved": round(lane_ops / kstep_s / 1e12, 2),
+            "peak": FP64_VALU_PEAK_TFLOPS / 2,
+            "unit": "T fp64 VALU lane-ops/s",
+            "frac": round(lane_ops / kstep_s / 1e12 / (FP64_VALU_PEAK_TFLOPS / 2), 4),
+            "traffic": None,
+            "kernel": "personalized_kernel<float, " + ("PF_FMA" if fused else "PF_MULADD") + ">",
+            "kernel_ms_per_step": round(kstep_s * 1e3, 4),
+            "launches": launches,
+            "hbm_GBps": round(job_bytes / kstep_s / 1e9, 1),
+        },
+        "probe": probe,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -> tuple[float | None, str | None]:
     """HBM bytes per launch of the same kernel and workload from the newest committed
     rocprofv3 PMC summary (scripts/profile.sh -> profiles/<tag>_traffic.json), or None."""
@@ -237,7 +371,12 @@ def main() -> int:
     ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
+    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized"],
+                    help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU)")
+    ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
     args = ap.parse_args()
+    if args.workload == "personalized":
+        return main_personalized(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

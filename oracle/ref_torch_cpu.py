@@ -43,3 +43,37 @@ class RefOpsFedAvg:
             assert not out[k].isnan().any().cpu()
         self.acc, self.totals = {}, {}
         return out
+
+
+class RefOpsPersonalized:
+    """The reference's PersonalizedFedAVG op sequence (personalized_aggregation_algorithm.py:23-57)
+    in torch CPU ops, for bench.py's personalized cpu_baseline: every arrival is deep-copied into
+    each other receiver's FedAvg (copy.deepcopy, :38-40) and folded there (RefOpsFedAvg above);
+    the centralized model is the equal-weight weighted_avg of the receivers' results (:51-53,
+    aggregation_algorithm.py:63-74)."""
+
+    def __init__(self, worker_weights: dict[int, dict[int, float]]) -> None:
+        self.worker_weights = worker_weights
+        self.algos = {j: RefOpsFedAvg() for j in worker_weights}
+
+    def add(self, worker_id: int, parameter: dict[str, torch.Tensor]) -> None:
+        for j, algo in self.algos.items():
+            if j == worker_id:
+                continue
+            copy = {k: v.clone() for k, v in parameter.items()}  # copy.deepcopy of the message
+            algo.add(copy, self.worker_weights[j].get(worker_id, 0))
+
+    def finish(self) -> tuple[dict[int, dict[str, torch.Tensor]], dict[str, torch.Tensor]]:
+        results = {j: a.finish() for j, a in self.algos.items()}
+        c = 1 / len(results)
+        central: dict[str, torch.Tensor] = {}
+        for r in results.values():
+            d = {k: v.to(dtype=torch.float64) * c for k, v in r.items()}
+            if not central:
+                central = d
+            else:
+                for k in central:
+                    central[k] += d[k]
+        for v in central.values():
+            assert not v.isnan().any().cpu()
+        return results, central

@@ -363,7 +363,9 @@ def main() -> int:
     ap.add_argument("--layout", default="resnet18", choices=sorted(LAYOUTS))
     ap.add_argument("--clients-per-gpu", type=int, default=64)
     ap.add_argument("--wave", type=int, default=0, help="clients per launch (streaming waves); 0 = all")
-    ap.add_argument("--chunks", type=int, default=2)
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="tile chunks of the sharded reduce (0 = auto: 4 when world > 1 — "
+                         "the RCCL reduce of chunk c overlaps the partial of chunk c+1, DESIGN.md §5)")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -390,6 +392,8 @@ def main() -> int:
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
     sharded = world > 1 or args.force_collective
+    if args.chunks <= 0:
+        args.chunks = 4 if world > 1 else 2
 
     in_dtype = getattr(torch, args.in_dtype)
     out_dtype = getattr(torch, args.out_dtype)

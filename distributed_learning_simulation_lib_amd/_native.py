@@ -109,6 +109,9 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_pers_prof_enable": (c_int32, [c_void_p, c_int32]),
     "fedavg_pers_prof_collect": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
     "fedavg_fp64_probe": (c_int32, [c_int64, c_int32, _PD, c_void_p]),
+    # host ingest (host_pack.cpp)
+    "fedavg_host_pack": (c_int32, [c_void_p, _PP, POINTER(c_int64), POINTER(c_int64), c_int32]),
+    "fedavg_host_pack_threads": (c_int32, []),
 }
 
 _lib: ctypes.CDLL | None = None

@@ -73,6 +73,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__row: dict[str, tuple[torch.Tensor, Any]] = {}
         self.__has_data = False
         self.__ingest: HostIngest | None = None
+        self.__result_flat: torch.Tensor | None = None
 
     # ---- setup -------------------------------------------------------------------------
     @property
@@ -259,6 +260,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
 
     # ---- end of round (fed_avg_algorithm.py:76-113) ------------------------------------
     def _aggregate_parameter(self, chosen_worker_ids: set[int] | None = None) -> ModelParameter:
+        self.__result_flat = None
         if not self.accumulate:
             worker_data: MutableMapping[int, Message] = self._all_worker_data
             if chosen_worker_ids is not None:
@@ -279,8 +281,25 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__has_data = False
         out = {name: result[name] for name in layout.names}
         if self.result_device is not None:
-            out = {k: v.to(self.result_device) for k, v in out.items()}
+            out = self._move_result(out)
         return out
+
+    def _move_result(self, out: ModelParameter) -> ModelParameter:
+        """Results to ``result_device``: the native part lives in one flat device buffer, so a
+        host destination takes ONE device-to-host copy of it (not one per tensor)."""
+        assert self.result_device is not None
+        flat = self.__result_flat
+        if self.result_device.type != "cpu" or flat is None:
+            return {k: v.to(self.result_device) for k, v in out.items()}
+        host = flat.to(self.result_device)
+        moved: ModelParameter = {}
+        for name, v in out.items():
+            if v.numel() and v.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr():
+                off = v.storage_offset() - flat.storage_offset()
+                moved[name] = host[off : off + v.numel()].view(v.shape)
+            else:
+                moved[name] = v.to(self.result_device)
+        return moved
 
     def _finish_native(self) -> ModelParameter:
         ctx = self._context()
@@ -294,6 +313,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         out_dtype = torch.float64 if custom_divide else self.result_dtype
         flat = torch.empty(native.padded_offsets(8 if out_dtype == torch.float64 else 4)[1],
                            dtype=out_dtype, device=self.device)
+        self.__result_flat = None if custom_divide else flat
         offs, _ = native.padded_offsets(flat.element_size())
         outs = [flat[o : o + n] for o, n in zip(offs, native.numels)]
         delta = self.__table_delta and table is not None

@@ -277,6 +277,17 @@ int32_t fedavg_pers_prof_collect(fedavg_pers* p, double* total_ms, int32_t* laun
 /* fp64 VALU ceiling probe (independent v_fma_f64 chains): measured TFLOP/s */
 int32_t fedavg_fp64_probe(int64_t waves, int32_t iters, double* tflops_out, void* stream);
 
+/* =====================================================================================
+ * Host ingest (aggregation_server.py:129: updates arrive as CPU tensors). Copy one client's
+ * n tensors (pageable host memory, srcs[i], nbytes[i]) into a pinned staging bucket at byte
+ * offsets dst_off[i], with a persistent pool of host threads (FEDAVG_PACK_THREADS, default
+ * min(OMP_NUM_THREADS or cores, 8)); the caller then moves the bucket with one DMA.
+ * Synchronous. A NULL source or 0 bytes is skipped.
+ * ===================================================================================== */
+int32_t fedavg_host_pack(void* dst, const void* const* srcs, const int64_t* nbytes, const int64_t* dst_off,
+                         int32_t n);
+int32_t fedavg_host_pack_threads(void);
+
 #ifdef __cplusplus
 }
 #endif

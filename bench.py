@@ -390,7 +390,11 @@ def main() -> int:
     if world > 1 or args.force_collective:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
+        # RCCL on a high-priority stream: its workgroups take free CU slots ahead of the next
+        # chunk's partial-kernel workgroups, so the reduce of chunk c starts under chunk c+1
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world, pg_options=opts)
     sharded = world > 1 or args.force_collective
     if args.chunks <= 0:
         args.chunks = 4 if world > 1 else 2

@@ -20,8 +20,8 @@ class OracleAlgorithm:
     def set_config(self, config) -> None:
         self.config = config
 
-    def set_old_parameter(self, old) -> None:
-        self.old = old
+    def set_old_parameter(self, old_parameter) -> None:
+        self.old = old_parameter
 
     def process_worker_data(self, worker_id, worker_data) -> bool:
         if worker_data is None:

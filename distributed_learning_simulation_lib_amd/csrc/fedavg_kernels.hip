@@ -76,6 +76,9 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_AE_HALF  // elements per lane for 2-byte inputs (fp16 / bf16)
 #define FEDAVG_AE_HALF 8
 #endif
+#ifndef FEDAVG_AE_F64  // elements per lane for fp64 inputs
+#define FEDAVG_AE_F64 16
+#endif
 #ifndef FEDAVG_TILE1  // elements per tile of the exact-order kernel (all dtypes)
 #define FEDAVG_TILE1 4096
 #endif
@@ -326,7 +329,8 @@ struct LaneLoader {
 // group) — the fastest shapes measured on MI355X. The split kernel keeps kAE for all dtypes.
 template <typename T, int SPLIT>
 struct Geo {
-  static constexpr int AE = (SPLIT > 1) ? kAE : (sizeof(T) == 2 ? FEDAVG_AE_HALF : kAE);
+  static constexpr int AE = (SPLIT > 1) ? kAE
+                          : (sizeof(T) == 2 ? FEDAVG_AE_HALF : sizeof(T) == 8 ? FEDAVG_AE_F64 : kAE);
   static constexpr int LANES = (SPLIT > 1) ? 64 : kTile1 / AE;
   static constexpr int THREADS = (SPLIT > 1) ? kThreads : LANES;
   static constexpr int TILE = LANES * AE;

@@ -366,6 +366,8 @@ def main() -> int:
     ap.add_argument("--chunks", type=int, default=0,
                     help="tile chunks of the sharded reduce (0 = auto: 4 when world > 1 — "
                          "the RCCL reduce of chunk c overlaps the partial of chunk c+1, DESIGN.md §5)")
+    ap.add_argument("--partial-streams", type=int, default=2,
+                    help="compute streams the chunk launches round-robin over (sharded path)")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -424,7 +426,7 @@ def main() -> int:
         out_flat = torch.empty(padded, dtype=out_dtype, device=device)
         outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
     reducer = HipLocalReducer(ctx, tables[-1], in_dtype, outs, out_dtype, prior_waves=tables[:-1],
-                              use_plan=not args.no_plan)
+                              use_plan=not args.no_plan, partial_streams=args.partial_streams)
     local_totals = [float(sum(my_weights))] * T
     global_totals = [float(sum(weights_all))] * T
 

@@ -69,6 +69,7 @@ class HipLocalReducer:
         out_dtype: torch.dtype,
         prior_waves: Sequence[ClientTable] = (),
         use_plan: bool = True,
+        partial_streams: int = 2,
     ) -> None:
         self.ctx = ctx
         self.use_plan = use_plan
@@ -83,6 +84,12 @@ class HipLocalReducer:
         self._finalize_plan = None
         self._finalize_totals: list[float] | None = None
         self.comm_stream = torch.cuda.Stream(ctx.device) if ctx.accumulator.is_cuda else None
+        # Extra compute streams for the chunk launches (round-robin with the current stream):
+        # chunk c+1's workgroups fill the CUs that chunk c's last pass of its persistent grid
+        # leaves idle. Only with prepared plans — a plan launch touches no shared context
+        # state, and the chunks write disjoint tile ranges.
+        self.side_streams = ([torch.cuda.Stream(ctx.device) for _ in range(max(0, partial_streams - 1))]
+                             if ctx.accumulator.is_cuda and use_plan else [])
 
     @property
     def num_tiles(self) -> int:
@@ -180,16 +187,23 @@ def sharded_reduce(
     works = []
     comm = getattr(reducer, "comm_stream", None)
     if acc.is_cuda and comm is not None:
-        # 1) every chunk's partial kernel goes into the compute stream back to back, each
-        #    followed by an event; 2) the reduces are issued from a side stream that waits only
+        # 1) every chunk's partial kernel goes into a compute stream (round-robin over the
+        #    reducer's streams), each followed by an event; 2) the reduces are issued from a side stream that waits only
         #    for its own chunk's event, so the reduce of chunk c runs under the partial of c+1
         compute = torch.cuda.current_stream(acc.device)
+        streams = [compute] + (list(getattr(reducer, "side_streams", [])) if len(bounds) > 1 else [])
+        for s in streams[1:]:
+            s.wait_stream(compute)  # the prefold / staging enqueued before this reduce
         events = []
-        for tb, te in bounds:
-            reducer.partial(tb, te)
+        for i, (tb, te) in enumerate(bounds):
+            s = streams[i % len(streams)]
+            with torch.cuda.stream(s):
+                reducer.partial(tb, te)
             ev = torch.cuda.Event()
-            ev.record(compute)
+            ev.record(s)
             events.append(ev)
+        for s in streams[1:]:
+            compute.wait_stream(s)  # finalize / the next round come after every chunk
         with torch.cuda.stream(comm):
             for (tb, te), ev in zip(bounds, events):
                 comm.wait_event(ev)

@@ -366,8 +366,6 @@ def main() -> int:
     ap.add_argument("--chunks", type=int, default=0,
                     help="tile chunks of the sharded reduce (0 = auto: 4 when world > 1 — "
                          "the RCCL reduce of chunk c overlaps the partial of chunk c+1, DESIGN.md §5)")
-    ap.add_argument("--partial-streams", type=int, default=2,
-                    help="compute streams the chunk launches round-robin over (sharded path)")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -426,13 +424,17 @@ def main() -> int:
         out_flat = torch.empty(padded, dtype=out_dtype, device=device)
         outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
     reducer = HipLocalReducer(ctx, tables[-1], in_dtype, outs, out_dtype, prior_waves=tables[:-1],
-                              use_plan=not args.no_plan, partial_streams=args.partial_streams)
+                              use_plan=not args.no_plan)
     local_totals = [float(sum(my_weights))] * T
     global_totals = [float(sum(weights_all))] * T
 
+    host_enqueue = [0.0]  # host time to enqueue one round (diagnostic: is the step host-bound?)
+
     def step() -> None:
+        h0 = time.perf_counter()
         sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals,
                        force_collective=args.force_collective)
+        host_enqueue[0] += time.perf_counter() - h0
         if rank == 0:
             ctx.raise_on_nan()  # the reference's assertions: the round ends on the host
 
@@ -442,6 +444,7 @@ def main() -> int:
     if dist.is_initialized():
         dist.barrier()
     ctx.prof_collect()  # drop warmup events
+    host_enqueue[0] = 0.0
     ctx.prof_enable(True)
     torch.cuda.synchronize(device)
     if dist.is_initialized():
@@ -543,6 +546,7 @@ def main() -> int:
             "mean_launch_ms": round(per_launch_ms, 4),
             "launches": launches,
         },
+        "host_enqueue_ms_per_step": round(host_enqueue[0] * 1e3 / args.steps, 4),
         "hbm_probe": probe,
         "cpu_baseline": cpu,
     }

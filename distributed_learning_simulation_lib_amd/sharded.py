@@ -10,8 +10,9 @@ clients are partitioned over the ranks (one process per GPU, ``torch.distributed
     root:    out = S / W                                (HIP finalize kernel, per chunk)
 
 The partial is produced and reduced in chunks of tiles: the kernel for chunk c+1 runs on
-the compute stream while RCCL reduces chunk c on its own stream, and the root finalizes
-chunk c as soon as its reduce has landed. This is the only exchange step of the path.
+the compute stream while RCCL reduces chunk c on its own stream; the root finalizes every
+tile in one launch once the last reduce has landed. This is the only exchange step of the
+path.
 
 Numerics: each rank accumulates its clients in arrival order exactly like the single-GPU
 kernel; the cross-rank sum reorders fp64 additions, so results match the reference to fp64
@@ -69,7 +70,6 @@ class HipLocalReducer:
         out_dtype: torch.dtype,
         prior_waves: Sequence[ClientTable] = (),
         use_plan: bool = True,
-        partial_streams: int = 2,
     ) -> None:
         self.ctx = ctx
         self.use_plan = use_plan
@@ -83,13 +83,6 @@ class HipLocalReducer:
         self._partial_plan = None
         self._finalize_plan = None
         self._finalize_totals: list[float] | None = None
-        self.comm_stream = torch.cuda.Stream(ctx.device) if ctx.accumulator.is_cuda else None
-        # Extra compute streams for the chunk launches (round-robin with the current stream):
-        # chunk c+1's workgroups fill the CUs that chunk c's last pass of its persistent grid
-        # leaves idle. Only with prepared plans — a plan launch touches no shared context
-        # state, and the chunks write disjoint tile ranges.
-        self.side_streams = ([torch.cuda.Stream(ctx.device) for _ in range(max(0, partial_streams - 1))]
-                             if ctx.accumulator.is_cuda and use_plan else [])
 
     @property
     def num_tiles(self) -> int:
@@ -184,40 +177,23 @@ def sharded_reduce(
     reducer.prefold()
     bounds = chunk_bounds(reducer.num_tiles, chunks)
     acc = reducer.accumulator
+    # Each chunk's reduce is issued right after its partial kernel, from the compute stream:
+    # the process group's RCCL stream waits only for that chunk's kernel (an event on the
+    # compute stream) and reduces chunk c while the kernel for chunk c+1 runs. No intermediate
+    # "comm" stream: HIP maps streams onto a few hardware queues in order, and a wait parked
+    # in a queue shared with the compute stream would hold every reduce behind the last
+    # partial (kernel traces: scripts/gpu_sharded_trace.sh).
     works = []
-    comm = getattr(reducer, "comm_stream", None)
-    if acc.is_cuda and comm is not None:
-        # 1) every chunk's partial kernel goes into a compute stream (round-robin over the
-        #    reducer's streams), each followed by an event; 2) the reduces are issued from a side stream that waits only
-        #    for its own chunk's event, so the reduce of chunk c runs under the partial of c+1
-        compute = torch.cuda.current_stream(acc.device)
-        streams = [compute] + (list(getattr(reducer, "side_streams", [])) if len(bounds) > 1 else [])
-        for s in streams[1:]:
-            s.wait_stream(compute)  # the prefold / staging enqueued before this reduce
-        events = []
-        for i, (tb, te) in enumerate(bounds):
-            s = streams[i % len(streams)]
-            with torch.cuda.stream(s):
-                reducer.partial(tb, te)
-            ev = torch.cuda.Event()
-            ev.record(s)
-            events.append(ev)
-        for s in streams[1:]:
-            compute.wait_stream(s)  # finalize / the next round come after every chunk
-        with torch.cuda.stream(comm):
-            for (tb, te), ev in zip(bounds, events):
-                comm.wait_event(ev)
-                a, b = reducer.tile_range(tb, te)
-                works.append(dist.reduce(acc[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True))
-    else:
-        for tb, te in bounds:
-            reducer.partial(tb, te)
-            a, b = reducer.tile_range(tb, te)
-            works.append(dist.reduce(acc[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for tb, te in bounds:
+        reducer.partial(tb, te)
+        a, b = reducer.tile_range(tb, te)
+        works.append(dist.reduce(acc[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    # The collectives of one process group run on one RCCL stream and complete in issue
+    # order, so on the GPU one wait (the last reduce) covers every chunk: one cross-stream
+    # dependency instead of one per chunk. Host backends (gloo) wait for each work.
+    for w in (works[-1:] if acc.is_cuda else works):
+        w.wait()
     if rank == root:
         reducer.set_accumulated(global_totals)
-    for (tb, te), w in zip(bounds, works):
-        w.wait()
-        if rank == root:
-            reducer.finalize_range(tb, te)
+        reducer.finalize_range(0, reducer.num_tiles)  # one launch over every tile
     return global_totals

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Kernel timeline of the sharded path on one GPU (forced 1-rank RCCL reduce), for gap analysis.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+C=${1:-4}
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/strace_c${C} -o trace -- \
+  python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-probe --force-collective --chunks $C \
+  > gpurun_out/strace_c${C}.log 2>&1

@@ -45,7 +45,7 @@ from distributed_learning_simulation_lib_amd.fedavg import (  # noqa: E402
     OutputTable,
     bw_probe,
 )
-from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, sharded_reduce  # noqa: E402
+from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, RcclComm, sharded_reduce  # noqa: E402
 
 METRIC = "aggregated GB/s (device-resident), N-client weighted FedAvg reduce, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -366,6 +366,9 @@ def main() -> int:
     ap.add_argument("--chunks", type=int, default=0,
                     help="tile chunks of the sharded reduce (0 = auto: 4 when world > 1 — "
                          "the RCCL reduce of chunk c overlaps the partial of chunk c+1, DESIGN.md §5)")
+    ap.add_argument("--comm", default="native", choices=["native", "torch"],
+                    help="sharded path: the library's own RCCL communicator, whole round in one native "
+                         "call (native) or the chunks' reduces through torch.distributed (torch)")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -430,10 +433,12 @@ def main() -> int:
 
     host_enqueue = [0.0]  # host time to enqueue one round (diagnostic: is the step host-bound?)
 
+    comm = RcclComm(device) if sharded and args.comm == "native" else None
+
     def step() -> None:
         h0 = time.perf_counter()
         sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals,
-                       force_collective=args.force_collective)
+                       force_collective=args.force_collective, comm=comm)
         host_enqueue[0] += time.perf_counter() - h0
         if rank == 0:
             ctx.raise_on_nan()  # the reference's assertions: the round ends on the host
@@ -495,6 +500,9 @@ def main() -> int:
         torch.cuda.empty_cache()
         cpu = cpu_baseline(layout)
 
+    if comm is not None:
+        torch.cuda.synchronize(device)
+        comm.close()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
@@ -527,6 +535,7 @@ def main() -> int:
             "accumulate_dtype": "float64",
             "out_dtype": args.out_dtype,
             "parallelism": "single GPU" if world == 1 else f"clients sharded over {world} GPUs + chunked RCCL reduce to rank 0",
+            "exchange": None if not sharded else {"chunks": args.chunks, "comm": args.comm},
             "baseline_config": ("BASELINE.json configs[1]" if (world == 1 and args.layout == "resnet18" and n_local == 64)
                                 else "BASELINE.json configs[2] (weak-scaled, 64 clients/GPU)" if args.layout == "resnet18"
                                 else "see DESIGN.md"),

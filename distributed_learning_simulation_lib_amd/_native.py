@@ -24,6 +24,8 @@ ERR_NAN_RESULT = 3
 ERR_INVALID = 4
 ERR_HIP = 5
 ERR_STATE = 6
+ERR_RCCL = 7
+COMM_ID_BYTES = 128
 FLAG_ACC_NAN = 0x1
 FLAG_RESULT_NAN = 0x2
 FLAG_CENTRAL_NAN = 0x4
@@ -112,6 +114,10 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     # host ingest (host_pack.cpp)
     "fedavg_host_pack": (c_int32, [c_void_p, _PP, POINTER(c_int64), POINTER(c_int64), c_int32]),
     "fedavg_host_pack_threads": (c_int32, []),
+    "fedavg_comm_unique_id": (c_int32, [c_void_p]),
+    "fedavg_comm_create": (c_int32, [_PP, c_void_p, c_int32, c_int32, c_int32]),
+    "fedavg_comm_destroy": (c_int32, [c_void_p]),
+    "fedavg_sharded_round": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
 }
 
 _lib: ctypes.CDLL | None = None

@@ -19,7 +19,8 @@ CSRC = PKG_DIR / "csrc"
 LIB_DIR = PKG_DIR / "_lib"
 LIB_NAME = "libfedavg_hip.so"
 LIB_PATH = LIB_DIR / LIB_NAME
-SOURCES = [CSRC / "fedavg_kernels.hip", CSRC / "personalized_kernels.hip", CSRC / "host_pack.cpp"]
+SOURCES = [CSRC / "fedavg_kernels.hip", CSRC / "personalized_kernels.hip", CSRC / "host_pack.cpp",
+           CSRC / "sharded_comm.cpp"]
 HEADERS = [REPO_DIR / "include" / "fedavg_hip.h"]
 
 # -ffp-contract=off: the reference rounds the fp64 product and the fp64 sum separately

@@ -1,0 +1,205 @@
+// sharded_comm.cpp — the multi-GPU exchange step of the FedAvg reduce, owned by the library.
+//
+// clients are sharded over one process per GPU; every rank folds its
+// shard into an fp64 partial (the partial plan of fedavg_kernels.hip), the partials are summed to
+// a root over RCCL (xGMI), and the root divides by the global total weights (the finalize plan).
+// The reference has no collective (everything goes to one server process,
+// simulation_lib/server/aggregation_server.py:111-145); this is the only exchange of the path.
+//
+// One round, all enqueued from one host call (no per-chunk framework dispatch):
+//
+//   compute stream : partial[c0] ev0  partial[c1] ev1 ...  partial[cK-1] evK-1  (wait done) finalize
+//   comm stream    :   (wait ev0) reduce[c0]  (wait ev1) reduce[c1] ...  reduce[cK-1] done
+//
+// The comm stream is a high-priority stream of its own: HIP places it on another hardware queue
+// than the compute stream, so its waits do not sit behind later partial kernels (an AQL queue is
+// processed in order; DESIGN.md §5 has the kernel traces). RCCL is not linked: the library binds
+// the RCCL the process already has (torch's, by SONAME librccl.so.1) or loads it, at
+// communicator creation (dlopen/dlsym). rccl.h supplies the types only.
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fedavg_hip.h"
+
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_fail(int32_t code, const char* msg);
+
+namespace {
+
+struct Rccl {
+  void* handle = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclReduce) reduce = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string error;
+};
+
+// The process's RCCL, bound once. RTLD_NOLOAD first: if torch (or the caller) has loaded an RCCL,
+// use that very library, so one process never carries two RCCL runtimes.
+Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* env = std::getenv("FEDAVG_RCCL_LIB");
+    const char* names[] = {env, "librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    for (const char* n : names) {
+      if (!n || !*n) continue;
+      r.handle = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
+      if (r.handle) break;
+    }
+    if (!r.handle) {
+      for (const char* n : names) {
+        if (!n || !*n) continue;
+        r.handle = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+        if (r.handle) break;
+      }
+    }
+    if (!r.handle) {
+      const char* e = dlerror();
+      r.error = std::string("cannot load RCCL: ") + (e ? e : "not found");
+      return;
+    }
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(r.handle, "ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(r.handle, "ncclCommInitRank"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.handle, "ncclCommDestroy"));
+    r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(r.handle, "ncclReduce"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.handle, "ncclGetErrorString"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.reduce || !r.error_string)
+      r.error = "RCCL library lacks a required symbol";
+  });
+  return r;
+}
+
+int32_t rccl_ready() {
+  Rccl& r = rccl();
+  if (!r.error.empty()) return fedavg_internal_fail(FEDAVG_ERR_RCCL, r.error.c_str());
+  return FEDAVG_OK;
+}
+
+int32_t rccl_fail(ncclResult_t res, const char* what) {
+  std::string m = std::string(what) + ": " + rccl().error_string(res);
+  return fedavg_internal_fail(FEDAVG_ERR_RCCL, m.c_str());
+}
+
+#define COMM_HIP_TRY(expr)                                                                          \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
+    if (e_ != hipSuccess)                                                                           \
+      return fedavg_internal_fail(FEDAVG_ERR_HIP, (std::string(#expr) + ": " + hipGetErrorString(e_)).c_str()); \
+  } while (0)
+
+}  // namespace
+
+struct fedavg_comm {
+  ncclComm_t nccl = nullptr;
+  int32_t world = 0;
+  int32_t rank = 0;
+  int32_t device = 0;
+  hipStream_t stream = nullptr;  // high-priority comm stream
+  std::vector<hipEvent_t> chunk_events;
+  hipEvent_t done = nullptr;
+};
+
+extern "C" {
+
+int32_t fedavg_comm_unique_id(void* id_out) {
+  if (!id_out) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null id buffer");
+  if (int32_t st = rccl_ready()) return st;
+  ncclUniqueId id;
+  ncclResult_t res = rccl().get_unique_id(&id);
+  if (res != ncclSuccess) return rccl_fail(res, "ncclGetUniqueId");
+  std::memcpy(id_out, id.internal, FEDAVG_COMM_ID_BYTES);
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_comm_create(fedavg_comm** out, const void* id, int32_t world, int32_t rank, int32_t device) {
+  if (!out || !id) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world || device < 0)
+    return fedavg_internal_fail(FEDAVG_ERR_INVALID, "bad world / rank / device");
+  if (int32_t st = rccl_ready()) return st;
+  COMM_HIP_TRY(hipSetDevice(device));
+  auto* c = new fedavg_comm();
+  c->world = world;
+  c->rank = rank;
+  c->device = device;
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    fedavg_comm_destroy(c);
+    return fedavg_internal_fail(FEDAVG_ERR_HIP, (std::string("comm stream: ") + hipGetErrorString(e)).c_str());
+  }
+  ncclUniqueId uid;
+  std::memcpy(uid.internal, id, FEDAVG_COMM_ID_BYTES);
+  ncclResult_t res = rccl().comm_init_rank(&c->nccl, world, uid, rank);  // collective over the ranks
+  if (res != ncclSuccess) {
+    c->nccl = nullptr;
+    fedavg_comm_destroy(c);
+    return rccl_fail(res, "ncclCommInitRank");
+  }
+  *out = c;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_comm_destroy(fedavg_comm* c) {
+  if (!c) return FEDAVG_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->nccl) (void)rccl().comm_destroy(c->nccl);
+  for (hipEvent_t ev : c->chunk_events) (void)hipEventDestroy(ev);
+  if (c->done) (void)hipEventDestroy(c->done);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                             int32_t chunks, int32_t root, void* stream) {
+  if (!c || !ctx || !partial) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
+  if (root < 0 || root >= c->world) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "bad root");
+  if (c->rank == root && !finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "root needs a finalize plan");
+  const int32_t n = fedavg_num_tiles(ctx);
+  if (n <= 0) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "context has no tiles");
+  chunks = std::max(1, std::min(chunks, n));
+  COMM_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  while (static_cast<int32_t>(c->chunk_events.size()) < chunks) {
+    hipEvent_t ev = nullptr;
+    COMM_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->chunk_events.push_back(ev);
+  }
+  double* acc = static_cast<double*>(fedavg_accumulator(ctx));
+  int32_t tb = 0;
+  for (int32_t k = 0; k < chunks; ++k) {
+    const int32_t te = static_cast<int32_t>((static_cast<int64_t>(n) * (k + 1)) / chunks);
+    if (te <= tb) continue;
+    if (int32_t st = fedavg_plan_run_range(partial, tb, te, s)) return st;
+    int64_t a = 0, b = 0;
+    if (int32_t st = fedavg_tile_range(ctx, tb, te, &a, &b)) return st;
+    COMM_HIP_TRY(hipEventRecord(c->chunk_events[k], s));
+    COMM_HIP_TRY(hipStreamWaitEvent(c->stream, c->chunk_events[k], 0));
+    ncclResult_t res = rccl().reduce(acc + a, acc + a, static_cast<size_t>(b - a), ncclFloat64, ncclSum, root,
+                                     c->nccl, c->stream);
+    if (res != ncclSuccess) return rccl_fail(res, "ncclReduce");
+    tb = te;
+  }
+  // the compute stream goes on once the last reduce has landed (the reduces run in order)
+  COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
+  COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
+  if (c->rank == root) return fedavg_plan_run_range(finalize, 0, n, s);
+  return FEDAVG_OK;
+}
+
+}  // extern "C"

@@ -26,12 +26,14 @@ chunking / collective / finalize logic without a GPU.
 
 from __future__ import annotations
 
+import ctypes
 from collections.abc import Sequence
 from typing import Protocol
 
 import torch
 import torch.distributed as dist
 
+from . import _native
 from .fedavg import ClientTable, FedAvgContext, OutputTable
 
 
@@ -126,6 +128,19 @@ class HipLocalReducer:
         else:
             self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
 
+    def native_round(self, comm: RcclComm, total_weights: Sequence[float], chunks: int, root: int) -> None:
+        """One round through the library's own RCCL pipeline (``fedavg_sharded_round``): the
+        chunk launches, the reduces and the finalize are enqueued by one native call."""
+        assert self.use_plan and self.table is not None
+        if self._partial_plan is None:
+            self._partial_plan = self.ctx.plan_partial(self.table, self.in_dtype, zero_init=not self.prior_waves)
+        fin = None
+        if comm.rank == root:
+            self.set_accumulated(total_weights)
+            fin = self._finalize_plan._h
+        _native.check(self.ctx._lib.fedavg_sharded_round(comm.handle, self.ctx._h, self._partial_plan._h, fin,
+                                                         chunks, root, self.ctx.stream))
+
     def fused(self) -> None:
         """Single-rank shortcut: fold + divide in the last wave's launch, no extra fp64 pass."""
         assert self.outs is not None
@@ -137,6 +152,44 @@ class HipLocalReducer:
             return
         self.prefold()
         self.ctx.aggregate(self.table, self.in_dtype, self.outs, self.out_dtype)
+
+
+class RcclComm:
+    """The library's own RCCL communicator (``fedavg_comm_*``), one per process / GPU.
+
+    Rank 0 of ``group`` makes the RCCL unique id; it is shipped to the other ranks over the
+    existing process group (any backend), then every rank joins (collective). The library binds
+    the process's RCCL (torch's) at run time; see ``sharded_comm.cpp``.
+    """
+
+    def __init__(self, device: torch.device, group: dist.ProcessGroup | None = None) -> None:
+        self._lib = _native.load()
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = device
+        uid = torch.zeros(_native.COMM_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            _native.check(self._lib.fedavg_comm_unique_id(ctypes.c_void_p(uid.data_ptr())))
+        on_device = dist.get_backend(group) == "nccl"
+        t = uid.to(device) if on_device else uid
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(t, src=src, group=group)
+        uid = t.cpu() if on_device else t
+        h = ctypes.c_void_p()
+        _native.check(self._lib.fedavg_comm_create(ctypes.byref(h), ctypes.c_void_p(uid.data_ptr()), self.world,
+                                                   self.rank, device.index or 0))
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self._lib.fedavg_comm_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self) -> None:  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def chunk_bounds(num_tiles: int, chunks: int) -> list[tuple[int, int]]:
@@ -153,6 +206,7 @@ def sharded_reduce(
     group: dist.ProcessGroup | None = None,
     global_total_weights: Sequence[float] | None = None,
     force_collective: bool = False,
+    comm: RcclComm | None = None,
 ) -> list[float]:
     """One FedAvg reduce over every rank's shard; the result lands in the root's outputs.
 
@@ -161,7 +215,9 @@ def sharded_reduce(
     knows every client's weight) it passes ``global_total_weights`` and no collective is
     spent on them; otherwise they are all-reduced first. Returns the global totals. On a
     one-rank world the fused single-launch kernel is used (no fp64 round trip) unless
-    ``force_collective`` (tests / measurement of the sharded path on one GPU).
+    ``force_collective`` (tests / measurement of the sharded path on one GPU). With ``comm``
+    (the library's own RCCL communicator) a HIP reducer runs the whole round in one native call
+    (``fedavg_sharded_round``); otherwise the chunks' reduces go through ``torch.distributed``.
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1 and not (force_collective and dist.is_initialized()):
@@ -175,6 +231,9 @@ def sharded_reduce(
         global_total_weights = totals.tolist()
     global_totals = [float(w) for w in global_total_weights]
     reducer.prefold()
+    if comm is not None and hasattr(reducer, "native_round"):
+        reducer.native_round(comm, global_totals, chunks, root)
+        return global_totals
     bounds = chunk_bounds(reducer.num_tiles, chunks)
     acc = reducer.accumulator
     # Each chunk's reduce is issued right after its partial kernel, from the compute stream:

@@ -67,6 +67,7 @@ enum fedavg_status {
   FEDAVG_ERR_INVALID = 4,      /* bad argument / dtype / size */
   FEDAVG_ERR_HIP = 5,          /* HIP runtime error */
   FEDAVG_ERR_STATE = 6,        /* e.g. aggregate with nothing accumulated (:88 assert) */
+  FEDAVG_ERR_RCCL = 7,         /* RCCL missing or a collective failed (sharded path) */
 };
 
 /* flag bits latched by the kernels (read through fedavg_check) */
@@ -287,6 +288,30 @@ int32_t fedavg_fp64_probe(int64_t waves, int32_t iters, double* tflops_out, void
 int32_t fedavg_host_pack(void* dst, const void* const* srcs, const int64_t* nbytes, const int64_t* dst_off,
                          int32_t n);
 int32_t fedavg_host_pack_threads(void);
+
+/* =====================================================================================
+ * Multi-GPU exchange step (replaces nothing in the reference, which
+ * sends every update to one server process: aggregation_server.py:111-145). One process per
+ * GPU; the library owns an RCCL communicator (bound at run time from the process's RCCL,
+ * librccl.so.1 — torch's when torch is loaded; FEDAVG_RCCL_LIB overrides).
+ *   rank 0: fedavg_comm_unique_id(id); the caller ships the FEDAVG_COMM_ID_BYTES to every rank
+ *   every rank: fedavg_comm_create(&comm, id, world, rank, device)   (collective)
+ *   every round: fedavg_sharded_round(comm, ctx, partial_plan, finalize_plan_or_NULL, chunks,
+ *                root, stream)
+ * A round launches the partial plan in `chunks` tile ranges on `stream`; after each range its
+ * fp64 partial is summed into the root's accumulator by ncclReduce on the communicator's
+ * high-priority stream (overlapping the next range's kernel); `stream` then waits for the last
+ * reduce and the root runs the finalize plan over every tile. Asynchronous; check with
+ * fedavg_check on the root. Results: each rank's fold is exact, the cross-rank fp64 sum is
+ * RCCL's order.
+ * ===================================================================================== */
+#define FEDAVG_COMM_ID_BYTES 128
+typedef struct fedavg_comm fedavg_comm;
+int32_t fedavg_comm_unique_id(void* id_out);
+int32_t fedavg_comm_create(fedavg_comm** out, const void* id, int32_t world, int32_t rank, int32_t device);
+int32_t fedavg_comm_destroy(fedavg_comm* comm);
+int32_t fedavg_sharded_round(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                             int32_t chunks, int32_t root, void* stream);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 C=${1:-4}
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/strace_c${C} -o trace -- \
-  python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-probe --force-collective --chunks $C \
-  > gpurun_out/strace_c${C}.log 2>&1
+M=${2:-native}
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/strace_c${C}_${M} -o trace -- \
+  python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-probe --force-collective --chunks $C --comm $M \
+  > gpurun_out/strace_c${C}_${M}.log 2>&1

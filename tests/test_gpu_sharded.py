@@ -12,7 +12,7 @@ import torch
 import torch.distributed as dist
 
 from distributed_learning_simulation_lib_amd.fedavg import ClientTable, FedAvgContext, ModelLayout
-from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, sharded_reduce
+from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, RcclComm, sharded_reduce
 
 pytestmark = pytest.mark.gpu
 
@@ -32,8 +32,9 @@ def nccl_group(hip_device):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("native", [False, True])
 @pytest.mark.parametrize("chunks", [1, 3, 8])
-def test_forced_collective_matches_fused(chunks, hip_device, nccl_group):
+def test_forced_collective_matches_fused(chunks, native, hip_device, nccl_group):
     rng = np.random.default_rng(chunks)
     layout = ModelLayout(names=("a", "b", "c"), shapes=((70001,), (33, 65), (9000,)))
     g = torch.Generator().manual_seed(chunks)
@@ -50,9 +51,33 @@ def test_forced_collective_matches_fused(chunks, hip_device, nccl_group):
 
     ctx_b = FedAvgContext(layout, hip_device)
     out_b = [torch.empty(n, dtype=torch.float64, device=hip_device) for n in layout.numels]
-    got = sharded_reduce(HipLocalReducer(ctx_b, table, torch.float32, out_b, torch.float64), totals,
-                         chunks=chunks, force_collective=True)
-    assert got == totals
-    ctx_b.raise_on_nan()
-    for a, b in zip(out_a, out_b):
-        assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+    comm = RcclComm(hip_device) if native else None
+    red = HipLocalReducer(ctx_b, table, torch.float32, out_b, torch.float64)
+    for _ in range(2):  # a second round reuses the plans and the communicator's events
+        for o in out_b:
+            o.fill_(float("nan"))
+        got = sharded_reduce(red, totals, chunks=chunks, force_collective=True, comm=comm)
+        assert got == totals
+        ctx_b.raise_on_nan()
+        for a, b in zip(out_a, out_b):
+            assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+    if comm is not None:
+        torch.cuda.synchronize(hip_device)
+        comm.close()
+
+
+def test_native_comm_rejects_bad_arguments(hip_device, nccl_group):
+    from distributed_learning_simulation_lib_amd import _native
+
+    comm = RcclComm(hip_device)
+    lib = _native.load()
+    # root out of range, and a root without a finalize plan
+    assert lib.fedavg_sharded_round(comm.handle, None, None, None, 1, 0, None) == _native.ERR_INVALID
+    layout = ModelLayout(names=("a",), shapes=((1000,),))
+    ctx = FedAvgContext(layout, hip_device)
+    table = ClientTable(1)
+    table.add_client([torch.ones(1000, device=hip_device)], [1.0])
+    plan = ctx.plan_partial(table, torch.float32, zero_init=True)
+    assert lib.fedavg_sharded_round(comm.handle, ctx._h, plan._h, None, 1, 5, None) == _native.ERR_INVALID
+    assert lib.fedavg_sharded_round(comm.handle, ctx._h, plan._h, None, 1, 0, None) == _native.ERR_INVALID
+    comm.close()

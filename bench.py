@@ -373,6 +373,8 @@ def main() -> int:
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="diagnostic: time the steps without per-launch HIP events (no roofline)")
     ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
@@ -450,7 +452,7 @@ def main() -> int:
         dist.barrier()
     ctx.prof_collect()  # drop warmup events
     host_enqueue[0] = 0.0
-    ctx.prof_enable(True)
+    ctx.prof_enable(not args.no_kernel_events)
     torch.cuda.synchronize(device)
     if dist.is_initialized():
         dist.barrier()
@@ -487,6 +489,15 @@ def main() -> int:
     kernel_step_s = kernel_ms * 1e-3 / args.steps
     achieved = rank_bytes / kernel_step_s / 1e9 if kernel_step_s > 0 else 0.0
     per_launch_ms = kernel_ms / max(launches, 1)
+    kname = {torch.float32: "float", torch.float16: "__half", torch.bfloat16: "bf16_t", torch.float64: "double"}[in_dtype]
+    kernel_desc = None
+    if comm is not None and n_waves == 1:
+        # native round: one timed launch per round, the first chunk's partial kernel (events
+        # around every chunk would put markers into the pipeline they measure)
+        a, b = ctx.tile_range(0, ctx.num_tiles // max(1, min(args.chunks, ctx.num_tiles)))
+        rank_bytes = (b - a) * (n_local * in_bytes + 8)
+        achieved = rank_bytes / (per_launch_ms * 1e-3) / 1e9 if launches else 0.0
+        kernel_desc = f"fedavg_tile_kernel<{kname}, OUT_ACC, 1, true, fma> (partial, first of {args.chunks} chunks)"
 
     traffic, traffic_src = (None, None)
     if not sharded and n_waves == 1 and args.layout == "resnet18":
@@ -509,7 +520,6 @@ def main() -> int:
     if rank != 0:
         return 0
     short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
-    kname = {torch.float32: "float", torch.float16: "__half", torch.bfloat16: "bf16_t", torch.float64: "double"}[in_dtype]
     line = {
         "metric": METRIC,
         "value": round(value_gbps, 2),
@@ -548,9 +558,9 @@ def main() -> int:
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": (f"fedavg_tile_kernel<{kname}, OUT_F32, 1, true, fma>" if not sharded and n_waves == 1
+            "kernel": kernel_desc or (f"fedavg_tile_kernel<{kname}, OUT_F32, 1, true, fma>" if not sharded and n_waves == 1
                        else f"fedavg_tile_kernel<{kname}, ...> x {n_waves} waves" + (" + RCCL reduce + finalize" if sharded else "")),
-            "bytes_per_step_this_rank": rank_bytes,
+            "bytes_per_timed_launch" if kernel_desc else "bytes_per_step_this_rank": rank_bytes,
             "kernel_ms_per_step": round(kernel_ms / args.steps, 4),
             "mean_launch_ms": round(per_launch_ms, 4),
             "launches": launches,

@@ -21,12 +21,14 @@
 //     and one atomicOr per wave that saw a NaN.
 //   * No MFMA: 0.25-0.5 flop per byte, the kernel is HBM-bound.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
 
 #include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -987,38 +989,49 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
   return FEDAVG_OK;
 }
 
+// Launches go through hipExtLaunchKernelGGL: an optional stop event is attached to the kernel's
+// own dispatch (its completion signal) instead of a separate marker packet — a marker between
+// two kernels costs ~6-16 µs of queue latency (DESIGN.md §5 traces); the sharded round's
+// per-chunk events use this.
 template <typename T, int OUT, int SPLIT, bool VEC>
-hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s) {
+hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int threads = Geo<T, SPLIT>::THREADS;
   if (fold == FOLD_FMA) {
-    hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA>), dim3(nblocks), dim3(threads), 0, s, a);
+    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA>), dim3(nblocks), dim3(threads), 0, s, e0,
+                          e1, 0, a);
   } else if (fold == FOLD_DELTA) {
     if constexpr (SPLIT == 1) {
-      hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA>), dim3(nblocks), dim3(threads), 0, s, a);
+      hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA>), dim3(nblocks), dim3(threads), 0, s,
+                            e0, e1, 0, a);
     } else {
       return hipErrorInvalidValue;  // delta calls run the exact-order kernel only
     }
   } else {
-    hipLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD>), dim3(nblocks), dim3(threads), 0, s, a);
+    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD>), dim3(nblocks), dim3(threads), 0, s,
+                          e0, e1, 0, a);
   }
   return hipGetLastError();
 }
 
 template <typename T, int OUT>
-hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s) {
+hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s, hipEvent_t e0,
+                        hipEvent_t e1) {
   if (split == 4) {
-    return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s) : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s);
+    return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s, e0, e1)
+               : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s, e0, e1);
   }
-  return vec ? launch_fold<T, OUT, 1, true>(a, fold, nblocks, s) : launch_fold<T, OUT, 1, false>(a, fold, nblocks, s);
+  return vec ? launch_fold<T, OUT, 1, true>(a, fold, nblocks, s, e0, e1)
+             : launch_fold<T, OUT, 1, false>(a, fold, nblocks, s, e0, e1);
 }
 
 template <int OUT>
-hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s) {
+hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s,
+                      hipEvent_t e0, hipEvent_t e1) {
   switch (in_dtype) {
-    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s);
-    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s);
-    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s);
-    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s);
+    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
+    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
+    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
+    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1033,8 +1046,11 @@ int choose_split(const fedavg_ctx* c, int kmax) {
 }
 
 // Launch the main kernel over tiles [tb, te) of the split-specific tile table.
+// done_ev (optional, in/out): an event the caller wants completed with this kernel. When
+// profiling is on, the profiling stop event is handed back in its place.
 int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_dtype, int out_kind,
-                    int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1) {
+                    int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1,
+                    hipEvent_t* done_ev = nullptr) {
   if (st.delta) split = 1;  // delta folds run the exact-order kernel only
   KArgs a;
   a.segs = c->d_segs;
@@ -1060,26 +1076,32 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   // exact-order kernel: persistent grid of at most (resident blocks) workgroups
   const int nblocks = (split == 1 && c->persistent_blocks > 0) ? std::min(a.num_tiles, c->persistent_blocks)
                                                                : a.num_tiles;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  // Profiling events are recorded as markers around the launch (the cheapest form measured:
+  // attaching start/stop events to the dispatch cost the fused step ~6 µs more); without
+  // profiling, a requested done event is attached to the dispatch itself (no marker).
+  hipEvent_t e1 = done_ev ? *done_ev : nullptr;
+  hipEvent_t m0 = nullptr, m1 = nullptr;
   if (c->prof) {
-    e0 = take_event(c);
-    e1 = take_event(c);
-    if (!e0 || !e1) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
-    FEDAVG_HIP_TRY(hipEventRecord(e0, s));
+    m0 = take_event(c);
+    m1 = take_event(c);
+    if (!m0 || !m1) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
+    FEDAVG_HIP_TRY(hipEventRecord(m0, s));
+    c->prof_events.emplace_back(m0, m1);
+    e1 = nullptr;
   }
   hipError_t err = hipSuccess;
   const int fold = st.delta ? FOLD_DELTA
                             : (c->allow_fma && fma_exact_call(st, in_dtype)) ? FOLD_FMA : FOLD_MULADD;
   switch (out_kind) {
-    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s); break;
-    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s); break;
-    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s); break;
+    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1); break;
+    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1); break;
+    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1); break;
     default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
   }
   if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
-  if (c->prof) {
-    FEDAVG_HIP_TRY(hipEventRecord(e1, s));
-    c->prof_events.emplace_back(e0, e1);
+  if (m1) {
+    FEDAVG_HIP_TRY(hipEventRecord(m1, s));
+    if (done_ev) *done_ev = m1;
   }
   return FEDAVG_OK;
 }
@@ -1678,6 +1700,30 @@ int32_t fedavg_plan_create_finalize(fedavg_ctx* c, const double* total_weights, 
   }
   *out = p;
   return FEDAVG_OK;
+}
+
+// Shared with sharded_comm.cpp: set the profiling flag, return the previous one (the sharded
+// round times one chunk launch per round: per-launch markers inside its chunk pipeline would
+// perturb what they measure).
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_set_prof(fedavg_ctx* c, int32_t on) {
+  const int32_t old = c->prof ? 1 : 0;
+  c->prof = on != 0;
+  return old;
+}
+
+// Shared with sharded_comm.cpp: a range launch whose completion also completes *done_ev
+// (attached to the kernel's dispatch; the profiling event replaces it when profiling is on).
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range(fedavg_plan* p, int32_t tb, int32_t te,
+                                                                           void* stream, hipEvent_t* done_ev) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind == fedavg_plan::AGGREGATE) return fail(FEDAVG_ERR_INVALID, "aggregate plans run whole (fedavg_plan_run)");
+  fedavg_ctx* c = p->ctx;
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (te < 0) te = n;
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, p->zero_init, tb, te,
+                     done_ev);
 }
 
 int32_t fedavg_plan_run_range(fedavg_plan* p, int32_t tb, int32_t te, void* stream) {

@@ -8,7 +8,7 @@
 //
 // One round, all enqueued from one host call (no per-chunk framework dispatch):
 //
-//   compute stream : partial[c0] ev0  partial[c1] ev1 ...  partial[cK-1] evK-1  (wait done) finalize
+//   compute stream : partial[c0]→ev0  partial[c1]→ev1 ...  partial[cK-1]→evK-1  (wait done) finalize
 //   comm stream    :   (wait ev0) reduce[c0]  (wait ev1) reduce[c1] ...  reduce[cK-1] done
 //
 // The comm stream is a high-priority stream of its own: HIP places it on another hardware queue
@@ -31,6 +31,9 @@
 #include "../../include/fedavg_hip.h"
 
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_fail(int32_t code, const char* msg);
+extern "C" __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range(
+    fedavg_plan* p, int32_t tb, int32_t te, void* stream, hipEvent_t* done_ev);
+extern "C" __attribute__((visibility("hidden"))) int32_t fedavg_internal_set_prof(fedavg_ctx* c, int32_t on);
 
 namespace {
 
@@ -181,15 +184,24 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
     c->chunk_events.push_back(ev);
   }
   double* acc = static_cast<double*>(fedavg_accumulator(ctx));
+  // with profiling on (fedavg_prof_enable), only the first chunk's launch is timed
+  const int32_t prof = fedavg_internal_set_prof(ctx, 0);
+  struct Restore {
+    fedavg_ctx* ctx;
+    int32_t prof;
+    ~Restore() { fedavg_internal_set_prof(ctx, prof); }
+  } restore{ctx, prof};
   int32_t tb = 0;
   for (int32_t k = 0; k < chunks; ++k) {
     const int32_t te = static_cast<int32_t>((static_cast<int64_t>(n) * (k + 1)) / chunks);
     if (te <= tb) continue;
-    if (int32_t st = fedavg_plan_run_range(partial, tb, te, s)) return st;
+    fedavg_internal_set_prof(ctx, (k == 0) ? prof : 0);
+    // the chunk's event completes with its kernel (no marker packet between chunk kernels)
+    hipEvent_t ev = c->chunk_events[k];
+    if (int32_t st = fedavg_internal_plan_run_range(partial, tb, te, s, &ev)) return st;
     int64_t a = 0, b = 0;
     if (int32_t st = fedavg_tile_range(ctx, tb, te, &a, &b)) return st;
-    COMM_HIP_TRY(hipEventRecord(c->chunk_events[k], s));
-    COMM_HIP_TRY(hipStreamWaitEvent(c->stream, c->chunk_events[k], 0));
+    COMM_HIP_TRY(hipStreamWaitEvent(c->stream, ev, 0));
     ncclResult_t res = rccl().reduce(acc + a, acc + a, static_cast<size_t>(b - a), ncclFloat64, ncclSum, root,
                                      c->nccl, c->stream);
     if (res != ncclSuccess) return rccl_fail(res, "ncclReduce");
@@ -198,6 +210,7 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
   // the compute stream goes on once the last reduce has landed (the reduces run in order)
   COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
   COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
+  fedavg_internal_set_prof(ctx, 0);
   if (c->rank == root) return fedavg_plan_run_range(finalize, 0, n, s);
   return FEDAVG_OK;
 }

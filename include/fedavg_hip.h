@@ -303,7 +303,8 @@ int32_t fedavg_host_pack_threads(void);
  * high-priority stream (overlapping the next range's kernel); `stream` then waits for the last
  * reduce and the root runs the finalize plan over every tile. Asynchronous; check with
  * fedavg_check on the root. Results: each rank's fold is exact, the cross-rank fp64 sum is
- * RCCL's order.
+ * RCCL's order. With profiling enabled on ctx, only the first chunk's launch of
+ * a round is timed (fedavg_prof_collect).
  * ===================================================================================== */
 #define FEDAVG_COMM_ID_BYTES 128
 typedef struct fedavg_comm fedavg_comm;

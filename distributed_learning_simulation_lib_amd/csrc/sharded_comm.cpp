@@ -207,7 +207,10 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
     if (res != ncclSuccess) return rccl_fail(res, "ncclReduce");
     tb = te;
   }
-  // the compute stream goes on once the last reduce has landed (the reduces run in order)
+  // The compute stream goes on once the last reduce has landed (the reduces run in order); the
+  // root then divides every tile in one launch. (Dividing each chunk on the comm stream right
+  // behind its reduce was measured slower: 0.595 vs 0.566 ms per one-rank round at 4 chunks —
+  // the finalize kernels contend with the next chunk's partial for CUs and HBM.)
   COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
   COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
   fedavg_internal_set_prof(ctx, 0);

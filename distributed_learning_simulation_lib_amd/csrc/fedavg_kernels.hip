@@ -1288,7 +1288,14 @@ int32_t fedavg_reset(fedavg_ctx* c, void* stream) {
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
-  FEDAVG_HIP_TRY(hipMemsetAsync(c->d_flag, 0, sizeof(uint32_t) * 4, static_cast<hipStream_t>(stream)));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipStreamQuery(s) == hipSuccess) {
+    // idle stream (the usual case: the previous round ended on the host): clear the host-coherent
+    // flag words directly — an async memset is a blit kernel plus ~15 µs of queue latency per round
+    for (int i = 0; i < 4; ++i) __atomic_store_n(&c->h_flag[i], 0u, __ATOMIC_RELEASE);
+  } else {
+    FEDAVG_HIP_TRY(hipMemsetAsync(c->d_flag, 0, sizeof(uint32_t) * 4, s));
+  }
   return FEDAVG_OK;
 }
 

@@ -22,6 +22,8 @@ LIB_PATH = LIB_DIR / LIB_NAME
 SOURCES = [CSRC / "fedavg_kernels.hip", CSRC / "personalized_kernels.hip", CSRC / "host_pack.cpp",
            CSRC / "sharded_comm.cpp"]
 HEADERS = [REPO_DIR / "include" / "fedavg_hip.h"]
+# C++ clients of the ABI alone (no Python, no torch), built next to the library
+EXAMPLES = {"c_abi_round": REPO_DIR / "examples" / "c_abi_round.cpp"}
 
 # -ffp-contract=off: the reference rounds the fp64 product and the fp64 sum separately
 # (torch `x.to(f64) * w` then `acc += tmp`); an FMA would change low bits.
@@ -57,6 +59,7 @@ def build(force: bool = False, verbose: bool = False, defines: dict[str, int] | 
     """
     target = out or LIB_PATH
     if out is None and not defines and not force and not needs_build():
+        build_examples(verbose=verbose)
         return LIB_PATH
     target.parent.mkdir(parents=True, exist_ok=True)
     tmp = target.with_suffix(".so.tmp")
@@ -68,7 +71,28 @@ def build(force: bool = False, verbose: bool = False, defines: dict[str, int] | 
     if proc.returncode != 0:
         raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
     os.replace(tmp, target)
+    if out is None:
+        build_examples(verbose=verbose)
     return target
+
+
+def build_examples(verbose: bool = False) -> list[Path]:
+    """Link each example against the in-tree library (rpath $ORIGIN: they live in _lib/)."""
+    built = []
+    for name, src in EXAMPLES.items():
+        exe = LIB_DIR / name
+        if exe.exists() and exe.stat().st_mtime > max(src.stat().st_mtime, LIB_PATH.stat().st_mtime):
+            built.append(exe)
+            continue
+        cmd = [hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", f"-I{REPO_DIR / 'include'}", str(src),
+               f"-L{LIB_DIR}", "-lfedavg_hip", "-Wl,-rpath,$ORIGIN", "-o", str(exe)]
+        if verbose:
+            print(" ".join(cmd))
+        proc = subprocess.run(cmd, capture_output=True, text=True)
+        if proc.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name} ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
+        built.append(exe)
+    return built
 
 
 if __name__ == "__main__":

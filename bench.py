@@ -435,7 +435,13 @@ def main() -> int:
 
     host_enqueue = [0.0]  # host time to enqueue one round (diagnostic: is the step host-bound?)
 
-    comm = RcclComm(device) if sharded and args.comm == "native" else None
+    comm = None
+    if sharded and args.comm == "native":
+        try:
+            comm = RcclComm(device)
+        except Exception as e:  # e.g. no RCCL symbols: the same schedule through torch.distributed
+            print(f"warning: native RCCL communicator unavailable ({e}); using --comm torch", file=sys.stderr)
+            args.comm = "torch"
 
     def step() -> None:
         h0 = time.perf_counter()

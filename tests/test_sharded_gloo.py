@@ -152,3 +152,57 @@ def test_chunk_bounds_partition_tiles():
             assert b[0][0] == 0 and b[-1][1] == n
             assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
             assert all(x[1] > x[0] for x in b)
+
+
+class _FakeCommLib:
+    """Stands in for the HIP library: rank 0's id bytes, and what each rank joined with."""
+
+    ID = bytes(range(7, 7 + 128))
+
+    def __init__(self):
+        self.joined = None
+
+    def fedavg_comm_unique_id(self, ptr):
+        import ctypes
+
+        ctypes.memmove(ptr.value, self.ID, len(self.ID))
+        return 0
+
+    def fedavg_comm_create(self, out, id_ptr, world, rank, device):
+        import ctypes
+
+        self.joined = (ctypes.string_at(id_ptr.value, 128), world, rank)
+        return 0
+
+    def fedavg_comm_destroy(self, h):
+        return 0
+
+
+def _comm_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from distributed_learning_simulation_lib_amd import _native, sharded
+
+        fake = _FakeCommLib()
+        _native.load = lambda path=None: fake  # the id exchange only: no RCCL on the CPU
+        comm = sharded.RcclComm(torch.device("cpu"))
+        q.put((rank, fake.joined, comm.world, comm.rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_comm_ships_rank0_id_to_every_rank():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, joined, w, r in got:
+        assert joined == (_FakeCommLib.ID, world, rank) and (w, r) == (world, rank)

@@ -343,6 +343,171 @@ def main_personalized(args: argparse.Namespace) -> int:
     return 0
 
 
+def make_qsgd_clients(layout: ModelLayout, n: int, device: torch.device, level: int = 255):
+    """n synthetic QSGD-quantised clients (fp32 codec), records resident in HBM: slots uniform in
+    [0, level], random sign bits, per-tensor norms |N(0,1)| — the byte stream a
+    StochasticQuantClientEndpoint worker sends (quantized_endpoint.py:96-99)."""
+    from distributed_learning_simulation_lib_amd.quantized import record_bytes, sign_offset
+
+    sizes = [record_bytes(m) for m in layout.numels]
+    offs = np.cumsum([0] + sizes[:-1]).tolist()
+    total = sum(sizes)
+    buckets = torch.zeros((n, total), dtype=torch.uint8, device=device)
+    g = torch.Generator(device=device)
+    hdr = torch.zeros(16, dtype=torch.uint8)
+    hdr[8:12] = torch.tensor([level], dtype=torch.int32).view(torch.uint8)
+    rng = np.random.default_rng(7)
+    for i in range(n):
+        g.manual_seed(4321 + i)
+        for o, m in zip(offs, layout.numels):
+            rec = buckets[i, o : o + record_bytes(m)]
+            h = hdr.clone()
+            h[0:8] = torch.tensor([abs(float(rng.standard_normal())) + 0.1], dtype=torch.float64).view(torch.uint8)
+            rec[0:16] = h.to(device)
+            rec[16 : 16 + m] = torch.randint(0, level + 1, (m,), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
+            so = sign_offset(m)
+            nb = (m + 7) // 8
+            rec[so : so + nb] = torch.randint(0, 256, (nb,), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
+    views = [[buckets[i, o : o + sz] for o, sz in zip(offs, sizes)] for i in range(n)]
+    return buckets, views, total
+
+
+def cpu_baseline_qsgd(layout: ModelLayout, budget_s: float = 12.0, sample_clients: int = 4) -> dict:
+    """The reference's server path for quantised updates on the host: QuantServerEndpoint.get
+    dequantises every tensor (x = norm * sign * slot / level in torch CPU ops,
+    quantized_endpoint.py:69-77), then FedAVGAlgorithm's op sequence (oracle/ref_torch_cpu.py)."""
+    sys.path.insert(0, str(REPO))
+    from oracle.ref_torch_cpu import RefOpsFedAvg
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    weights = dataset_size_weights(sample_clients)
+    g = torch.Generator().manual_seed(1234)
+    clients = []
+    for _ in range(sample_clients):
+        c = {}
+        for name, shape in zip(layout.names, layout.shapes):
+            m = int(np.prod(shape))
+            c[name] = (torch.rand((), generator=g).item() + 0.1,
+                       torch.randint(0, 256, (m,), generator=g, dtype=torch.uint8),
+                       torch.randint(0, 256, ((m + 7) // 8,), generator=g, dtype=torch.uint8), shape)
+        clients.append(c)
+    shifts = torch.arange(7, -1, -1, dtype=torch.uint8)
+    rec_bytes = sum(m + (m + 7) // 8 for m in layout.numels)
+    nbytes = sample_clients * rec_bytes + layout.total_numel * 4
+    times = []
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < budget_s and len(times) < 1000:
+        algo = RefOpsFedAvg()
+        t0 = time.perf_counter()
+        for c, w in zip(clients, weights):
+            dense = {}
+            for name, (norm, slots, packed, shape) in c.items():
+                sign = ((packed.unsqueeze(1) >> shifts) & 1).reshape(-1)[: slots.numel()].to(torch.float32) * 2 - 1
+                dense[name] = ((torch.tensor(norm, dtype=torch.float32) * sign) * slots.to(torch.float32) / 255).view(shape)
+            algo.add(dense, w)
+        out = {k: v.to(torch.float32) for k, v in algo.finish().items()}
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {
+        "value": round(nbytes / best / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (
+            f"{sample_clients} QSGD-quantised clients x ResNet-18 layout (fp32 codec, level 255): host "
+            f"dequantisation (unpack signs, norm * sign * slot / level) + the reference FedAvg op sequence "
+            f"in torch CPU, best of {len(times)} runs over {time.perf_counter() - t_start:.1f} s"
+        ),
+    }
+
+
+def main_qsgd(args: argparse.Namespace) -> int:
+    """--workload qsgd: one FedAvg round over QSGD-quantised client updates (the server behind
+    StochasticQuantServerEndpoint, quantized_endpoint.py:102-111) with the dequantisation fused
+    into the fold; records resident in HBM, one GPU."""
+    from distributed_learning_simulation_lib_amd.quantized import QSGD_F32
+
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(device)
+    layout = LAYOUTS[args.layout]()
+    P, T, N = layout.total_numel, layout.num_segments, args.clients_per_gpu
+    out_dtype = getattr(torch, args.out_dtype)
+    buckets, views, client_bytes = make_qsgd_clients(layout, N, device)
+    weights = dataset_size_weights(N)
+    table = ClientTable(T)
+    for row, w in zip(views, weights):
+        table.add_client(row, [w] * T)
+    ctx = FedAvgContext(layout, device)
+    offs, padded = layout.padded_offsets(torch.empty((), dtype=out_dtype).element_size())
+    out_flat = torch.empty(padded, dtype=out_dtype, device=device)
+    outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
+    plan = ctx.plan(table, QSGD_F32, outs, out_dtype)
+
+    def step() -> None:
+        plan.run()
+        ctx.raise_on_nan()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    ctx.prof_collect()
+    ctx.prof_enable(True)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    ctx.prof_enable(False)
+    kernel_ms, launches = ctx.prof_collect()
+    out_bytes = torch.empty((), dtype=out_dtype).element_size()
+    job_bytes = N * client_bytes + P * out_bytes  # every record byte the fold must read + the result
+    step_s = elapsed / args.steps
+    per_launch_s = kernel_ms * 1e-3 / max(launches, 1)
+    achieved = job_bytes / per_launch_s / 1e9
+    probe = None if args.no_probe else hbm_probes(device)
+    cpu = None
+    if not args.no_cpu_baseline:
+        del buckets, views, table, plan
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline_qsgd(layout)
+    line = {
+        "metric": "aggregated GB/s (device-resident), N-client weighted FedAvg reduce over QSGD-quantised updates",
+        "value": round(job_bytes / step_s / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "replicas only",
+        "vs_baseline": None,
+        "client_elements_per_s": round(N * P / step_s, 1),
+        "dtype": "f64",
+        "data": "synthetic QSGD records: slots uniform in [0, 255], random signs, norms |N(0,1)|+0.1; dataset-size weights",
+        "config": {"workload": f"fedavg_qsgd255_{args.layout}_{N}_clients", "clients": N, "params_per_client": P,
+                   "tensors_per_client": T, "record_bytes_per_client": client_bytes, "codec": "qsgd_f32 (level 255)",
+                   "accumulate_dtype": "float64", "out_dtype": args.out_dtype},
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": None,
+            "kernel": f"qsgd_tile_kernel<OUT_{'F32' if out_dtype == torch.float32 else 'F64'}, float, true>",
+            "bytes_per_launch": job_bytes,
+            "mean_launch_ms": round(per_launch_s * 1e3, 4),
+            "launches": launches,
+        },
+        "hbm_probe": probe,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -> tuple[float | None, str | None]:
     """HBM bytes per launch of the same kernel and workload from the newest committed
     rocprofv3 PMC summary (scripts/profile.sh -> profiles/<tag>_traffic.json), or None."""
@@ -378,12 +543,15 @@ def main() -> int:
     ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
-    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized"],
-                    help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU)")
+    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd"],
+                    help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU); "
+                         "qsgd: FedAvg over QSGD-quantised updates, dequantisation fused (one GPU)")
     ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
     args = ap.parse_args()
     if args.workload == "personalized":
         return main_personalized(args)
+    if args.workload == "qsgd":
+        return main_qsgd(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

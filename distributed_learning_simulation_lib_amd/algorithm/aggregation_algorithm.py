@@ -19,6 +19,7 @@ import torch
 
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout
 from ..message import Message, ModelParameter, ParameterMessage
+from ..quantized import QuantizedTensor, dequantize_tensor
 
 # (device index, layout, split policy) -> context, for the class-level weighted_avg
 _CTX_CACHE: OrderedDict[tuple[int, ModelLayout, int], FedAvgContext] = OrderedDict()
@@ -158,12 +159,20 @@ class AggregationAlgorithm(ABC):
             assert 0 <= r <= 1
             assert isinstance(msg, ParameterMessage)
             assert msg.parameter
-            rows.append([to_device_operand(msg.parameter[name], device) for name in layout.names])
+            rows.append([msg.parameter[name] for name in layout.names])
             ratios.append(float(r))
         result: ModelParameter = {}
         if native is not None:
             flat = [rows[k][i] for k in range(len(rows)) for i in keep]
-            flat, dt = unify_dtype(flat)
+            codecs = {t.codec for t in flat if isinstance(t, QuantizedTensor)}
+            if len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in flat):
+                # QSGD records: dequantised inside the kernel (quantized.py)
+                dt = codecs.pop()
+                flat = [t.record.to(device) for t in flat]
+            else:
+                flat = [to_device_operand(dequantize_tensor(t) if isinstance(t, QuantizedTensor) else t, device)
+                        for t in flat]
+                flat, dt = unify_dtype(flat)
             T = len(keep)
             table = ClientTable(T)
             for k in range(len(rows)):

@@ -34,6 +34,7 @@ import torch
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
 from ..message import DeltaParameterMessage, Message, ModelParameter, ParameterMessage
+from ..quantized import QuantizedTensor, dequantize_tensor, record_layout
 from .aggregation_algorithm import (
     AggregationAlgorithm,
     default_device,
@@ -205,14 +206,23 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             else:
                 tensors.append(None)
                 weights.append(0.0)
-        tensors = self._to_device_row(tensors)
         present = [t for t in tensors if t is not None]
-        if present:
-            unified, dt = unify_dtype(present)
-            it = iter(unified)
-            tensors = [next(it) if t is not None else None for t in tensors]
+        codecs = {t.codec for t in present if isinstance(t, QuantizedTensor)}
+        if codecs and len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in present):
+            # quantised update: the records are the kernel operands (dequantised in the fold)
+            dt = codecs.pop()
+            tensors = self._records_to_device(tensors)
         else:
-            dt = self.__table_dtype or torch.float32
+            if codecs:  # mixed with dense tensors (e.g. complete()-d keys): dequantise here
+                tensors = [dequantize_tensor(t) if isinstance(t, QuantizedTensor) else t for t in tensors]
+            tensors = self._to_device_row(tensors)
+            present = [t for t in tensors if t is not None]
+            if present:
+                unified, dt = unify_dtype(present)
+                it = iter(unified)
+                tensors = [next(it) if t is not None else None for t in tensors]
+            else:
+                dt = self.__table_dtype or torch.float32
         if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
             self._flush()
         if self.__table is None:
@@ -244,6 +254,35 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 for t, m in zip(tensors, moved)
             ]
         return [None if t is None else to_device_operand(t, self.device) for t in tensors]
+
+    # Quantised updates (StochasticQuantServerEndpoint, quantized_endpoint.py:69-77,102-111) are
+    # handed over as QSGD records; the kernel dequantises them inside the fold.
+    accepts_quantized_messages = True
+
+    def _records_to_device(self, tensors: list) -> list[torch.Tensor | None]:
+        """One client's QSGD records in HBM: host records go through the pinned ingest (one
+        packed DMA per client), device records are used where they are."""
+        host = [q for q in tensors if q is not None and q.device.type == "cpu"]
+        moved: list[torch.Tensor | None] = [None] * len(tensors)
+        if host:
+            if self.__ingest is None:
+                self.__ingest = HostIngest(self.device)
+            numels = [q.numel if q is not None else 1 for q in tensors]
+            staged = self.__ingest.to_device(
+                record_layout(numels),
+                [q.record if q is not None and q.device.type == "cpu" else None for q in tensors],
+                torch.uint8,
+            )
+            moved = list(staged)
+        out: list[torch.Tensor | None] = []
+        for q, m in zip(tensors, moved):
+            if q is None:
+                out.append(None)
+            elif m is not None:
+                out.append(m)
+            else:
+                out.append(q.record if q.device == self.device else q.record.to(self.device))
+        return out
 
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""

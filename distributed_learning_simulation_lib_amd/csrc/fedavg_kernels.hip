@@ -671,6 +671,231 @@ __global__ __launch_bounds__((Geo<T, SPLIT>::THREADS), FEDAVG_MIN_WAVES) void fe
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Server-side dequantisation fused into the fold.
+//
+// The reference's StochasticQuantServerEndpoint.get (simulation_lib/topology/
+// quantized_endpoint.py:69-77, level 255 at :102-111) dequantises every arriving update on the
+// host — x = norm * sign * slot / level, per tensor (the QSGD codec of the unvendored
+// cyy_torch_algorithm.quantization.stochastic) — and FedAVGAlgorithm then folds the dense
+// copy (fed_avg_algorithm.py:54-58). Here the quantised record itself is the client "tensor":
+//
+//   record (16-B aligned, fedavg_qsgd_record_bytes(n) bytes, include/fedavg_hip.h):
+//     [0, 8)   norm (fp64; holds the fp32 norm exactly for FEDAVG_QSGD_F32)
+//     [8, 12)  level (int32, 1..255)
+//     [16, 16 + n)                          slots, one uint8 per element
+//     [16 + align16(n), ... + ceil(n / 8))  signs, numpy.packbits order (element i: byte
+//                                           i / 8, bit 7 - i % 8; 1 = non-negative)
+//
+// For one (client, tensor) the dequantised value depends only on (slot, sign), so the weighted
+// product the reference folds, round(f64(x) * w), takes at most 2 x 256 values: the workgroup
+// tabulates the 256 non-negative ones in LDS (one entry per lane, computed with the reference's
+// operation order in the codec's dtype) and every element folds acc + (sign ? p[slot] :
+// -p[slot]). The negative half is exact: every step (norm * ±1, * slot, / level, widening, * w)
+// rounds symmetrically. So the fold stays bit-identical to dequantise-then-FedAvg while HBM
+// carries 1.125 B per element per client instead of 4 (fp32) or 8 (fp64).
+//
+// Geometry: one 256-lane workgroup per 4096-element tile; lane li owns elements
+// [16 li, 16 li + 16) (one 16-B slot load + one 2-B sign load per client; a wave reads 1 KiB of
+// slots contiguously). Clients go in groups of QG: the group's loads are issued, its QG tables
+// are built into one of two LDS buffers, one barrier, then the fold in arrival order.
+constexpr int kQsgdGroup = 4;
+constexpr int kQsgdLanes = 256;
+constexpr int kQsgdAE = 16;
+
+template <typename DQ>
+__device__ __forceinline__ double qsgd_product(double norm, int level, int slot, double w) {
+  // torch evaluates `norm * sign * slot / level` left to right in the codec's dtype; with
+  // sign = +1 the first product is exact, so the non-negative value is (norm * slot) / level.
+  const DQ n = static_cast<DQ>(norm);
+  const DQ v = (n * static_cast<DQ>(slot)) / static_cast<DQ>(level);
+  const double x = static_cast<double>(v);  // .to(float64), fed_avg_algorithm.py:54
+  return x * w;
+}
+
+template <int OUT, typename DQ, bool FULL, bool VEC>
+__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][256]) {
+  constexpr int AE = kQsgdAE;
+  const int seg = td.seg;
+  const int count = td.count;
+  const int li = static_cast<int>(threadIdx.x);
+  const int e0 = li * AE;  // first element of this lane within the tile
+  const bool lane_live = FULL || e0 < count;
+
+  const int kseg = to_const<int32_t>(a.tab.kseg)[seg];
+  const kptr<uint64_t> cp = to_const<uint64_t>(a.tab.cptrs) + static_cast<int64_t>(seg) * a.K;
+  const kptr<double> wp = to_const<double>(a.tab.w) + static_cast<int64_t>(seg) * a.K;
+  const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;
+  const int64_t numel = to_const<int64_t>(a.segs)[2 * seg + 1];
+  const int64_t slot_off = 16 + td.start + e0;
+  const int64_t sign_off = 16 + ((numel + 15) & ~int64_t(15)) + (td.start + e0) / 8;
+
+  double acc[AE];
+#pragma unroll
+  for (int i = 0; i < AE; ++i) acc[i] = -0.0;  // additive identity (see tile_body)
+  bool have = a.zero_init != 0;
+  if (!a.zero_init && to_const<int32_t>(a.tab.acc_in)[seg]) {
+    const gptr<const double> ap = to_global<double>(a.acc + acc_base) + e0;
+#pragma unroll
+    for (int j = 0; j < AE; j += 2) {
+      if (FULL || e0 + j + 2 <= count) {
+        const f64x2 d = *(gptr<const f64x2>)(ap + j);
+        acc[j] = d.x;
+        acc[j + 1] = d.y;
+      } else {
+        if (e0 + j < count) acc[j] = ap[j];
+        if (e0 + j + 1 < count) acc[j + 1] = ap[j + 1];
+      }
+    }
+    have = true;
+  }
+
+  int buf = 0;
+  for (int k = 0; k < kseg; k += kQsgdGroup) {
+    const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
+    u32x4 slots[kQsgdGroup];
+    uint32_t signs[kQsgdGroup];
+    double nrm[kQsgdGroup], wk[kQsgdGroup];
+    int lvl[kQsgdGroup];
+#pragma unroll
+    for (int c = 0; c < kQsgdGroup; ++c) {
+      const int kc = k + min(c, n - 1);
+      const uint64_t rec = cp[kc];
+      const kptr<double> hdr = to_const<double>(reinterpret_cast<const void*>(rec));
+      nrm[c] = hdr[0];
+      lvl[c] = to_const<int32_t>(reinterpret_cast<const void*>(rec))[2];
+      wk[c] = wp[kc];
+      if (lane_live) {
+        const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(rec));
+#if FEDAVG_NT
+        slots[c] = __builtin_nontemporal_load((gptr<const u32x4>)(rp + slot_off));
+#else
+        slots[c] = *(gptr<const u32x4>)(rp + slot_off);
+#endif
+        signs[c] = *(gptr<const uint16_t>)(rp + sign_off);
+      } else {
+        slots[c] = u32x4{0u, 0u, 0u, 0u};
+        signs[c] = 0xffffu;
+      }
+    }
+    // this group's product tables: lane li tabulates slot value li of every client
+#pragma unroll
+    for (int c = 0; c < kQsgdGroup; ++c) lut[buf][c][li] = qsgd_product<DQ>(nrm[c], lvl[c], li, wk[c]);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kQsgdGroup; ++c) {
+      if (c < n) {
+        const double* tab = lut[buf][c];
+        // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte,
+        // element j >= 8 bit 15 - (j - 8) of the high byte of the little-endian 16-bit word
+#pragma unroll
+        for (int j = 0; j < AE; ++j) {
+          const uint32_t word = slots[c][j >> 2];
+          const uint32_t s = (word >> (8 * (j & 3))) & 0xffu;
+          const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
+          const bool pos = (signs[c] >> bit) & 1u;
+          const double p = tab[s];
+          acc[j] = acc[j] + (pos ? p : -p);
+        }
+      }
+    }
+    buf ^= 1;  // the next group writes the other buffer; the barrier above orders the reuse
+  }
+  have = have || (kseg > 0);
+  if (!have) return;
+
+  bool bad_acc = false;
+#pragma unroll
+  for (int j = 0; j < AE; ++j) bad_acc |= (FULL || e0 + j < count) && (acc[j] != acc[j]);
+
+  if constexpr (OUT == OUT_ACC) {
+    const gptr<double> ap = to_global_mut<double>(a.acc + acc_base) + e0;
+#pragma unroll
+    for (int j = 0; j < AE; j += 2) {
+      if (FULL || e0 + j + 2 <= count) {
+        *(gptr<f64x2>)(ap + j) = f64x2{acc[j], acc[j + 1]};
+      } else {
+        if (e0 + j < count) ap[j] = acc[j];
+        if (e0 + j + 1 < count) ap[j + 1] = acc[j + 1];
+      }
+    }
+    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) raise_flag(a.flag, 0);
+  } else {
+    const double W = to_const<double>(a.tab.wtot)[seg];
+    double res[AE];
+    bool bad_res = false;
+#pragma unroll
+    for (int j = 0; j < AE; ++j) {
+      res[j] = acc[j] / W;
+      bad_res |= (FULL || e0 + j < count) && (res[j] != res[j]);
+    }
+    void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
+    if constexpr (OUT == OUT_F32) {
+      const gptr<float> op = to_global_mut<float>(out_raw) + td.start + e0;
+#pragma unroll
+      for (int j = 0; j < AE; j += 4) {
+        if (VEC && (FULL || e0 + j + 4 <= count)) {
+          *(gptr<f32x4>)(op + j) = f32x4{static_cast<float>(res[j]), static_cast<float>(res[j + 1]),
+                                          static_cast<float>(res[j + 2]), static_cast<float>(res[j + 3])};
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (e0 + j + q < count) op[j + q] = static_cast<float>(res[j + q]);
+        }
+      }
+    } else {
+      const gptr<double> op = to_global_mut<double>(out_raw) + td.start + e0;
+#pragma unroll
+      for (int j = 0; j < AE; j += 2) {
+        if (VEC && (FULL || e0 + j + 2 <= count)) {
+          *(gptr<f64x2>)(op + j) = f64x2{res[j], res[j + 1]};
+        } else {
+          if (e0 + j < count) op[j] = res[j];
+          if (e0 + j + 1 < count) op[j + 1] = res[j + 1];
+        }
+      }
+    }
+    const uint64_t ba = __ballot(bad_acc);
+    const uint64_t br = __ballot(bad_res);
+    if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+      if (ba) raise_flag(a.flag, 0);
+      if (br) raise_flag(a.flag, 1);
+    }
+  }
+}
+
+template <int OUT, typename DQ, bool VEC>
+__global__ __launch_bounds__(kQsgdLanes) void qsgd_tile_kernel(KArgs a) {
+  __shared__ double lut[2][kQsgdGroup][256];
+  const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
+  if (td.count == kTile1) {
+    qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut);
+  } else {
+    qsgd_tile_body<OUT, DQ, false, VEC>(a, td, lut);
+  }
+}
+
+// Diagnostic for quantised clients: which record dequantises to a NaN somewhere.
+template <typename DQ>
+__global__ __launch_bounds__(kThreads) void qsgd_nan_scan_kernel(const TileDesc* tiles, const SegDesc* segs,
+                                                                const void* const* cptrs_tk, int32_t K,
+                                                                int32_t* bad) {
+  const TileDesc td = load_tile(tiles, blockIdx.x);
+  const int k = blockIdx.y;
+  const uint64_t raw = to_const<uint64_t>(cptrs_tk)[static_cast<int64_t>(td.seg) * K + k];
+  if (raw == 0) return;
+  const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(raw));
+  const double norm = *(gptr<const double>)rp;
+  const int level = *(gptr<const int32_t>)(rp + 8);
+  bool b = false;
+  for (int i = threadIdx.x; i < td.count; i += kThreads) {
+    const double x = qsgd_product<DQ>(norm, level, rp[16 + td.start + i], 1.0);
+    b |= (x != x);
+  }
+  (void)segs;
+  if (__ballot(b) != 0ull && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned*>(bad + k), 1u);
+}
+
 // Diagnostic: per-client "holds a NaN" flags (error path only, fed_avg_algorithm.py:35).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void nan_scan_kernel(const TileDesc* tiles,
@@ -789,6 +1014,8 @@ int32_t elem_size(int32_t dt) {
     case FEDAVG_F16: return 2;
     case FEDAVG_BF16: return 2;
     case FEDAVG_F64: return 8;
+    case FEDAVG_QSGD_F32: return 1;  // quantised records (slots are bytes)
+    case FEDAVG_QSGD_F64: return 1;
     default: return 0;
   }
 }
@@ -823,6 +1050,7 @@ struct Staged {
   int32_t Kmax = 0;
   int32_t stride = 1;    // row stride of the [T][K] tables
   bool aligned = true;
+  bool clients_aligned = true;  // every client pointer is 16-byte aligned
   bool delta = false;           // clients are deltas against tab.base (fp64)
   int32_t max_weight_bits = 0;  // largest significand (bits) among the call's weights
   bool weights_tame = true;     // every weight finite, zero or within [2^-800, 2^800]   // every client/out pointer is 16-byte aligned
@@ -919,13 +1147,14 @@ void build_blob(const fedavg_ctx* c, const void* const* client_ptrs, const doubl
   st.kseg.assign(T, 0);
   st.stride = Kr;
   st.aligned = true;
+  st.clients_aligned = true;
   st.Kmax = 0;
   for (int t = 0; t < T; ++t) {
     int n = 0;
     for (int k = 0; k < K; ++k) {
       const void* p = client_ptrs[static_cast<int64_t>(k) * T + t];
       if (p == nullptr) continue;
-      if (reinterpret_cast<uintptr_t>(p) % 16 != 0) st.aligned = false;
+      if (reinterpret_cast<uintptr_t>(p) % 16 != 0) st.aligned = st.clients_aligned = false;
       hp[static_cast<int64_t>(t) * Kr + n] = p;
       const double wv = weights[static_cast<int64_t>(k) * T + t];
       hw[static_cast<int64_t>(t) * Kr + n] = wv;
@@ -1036,6 +1265,21 @@ hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int
   }
 }
 
+bool is_qsgd(int32_t dt) { return dt == FEDAVG_QSGD_F32 || dt == FEDAVG_QSGD_F64; }
+
+template <int OUT>
+hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1) {
+  const dim3 grid(static_cast<unsigned>(a.num_tiles)), block(kQsgdLanes);
+  if (in_dtype == FEDAVG_QSGD_F32) {
+    if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true>), grid, block, 0, s, nullptr, e1, 0, a);
+    else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, false>), grid, block, 0, s, nullptr, e1, 0, a);
+  } else {
+    if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, double, true>), grid, block, 0, s, nullptr, e1, 0, a);
+    else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, double, false>), grid, block, 0, s, nullptr, e1, 0, a);
+  }
+  return hipGetLastError();
+}
+
 int choose_split(const fedavg_ctx* c, int kmax) {
   if (c->split_policy == 1) return 1;
   if (c->split_policy == 2) return kmax >= 4 ? 4 : 1;
@@ -1090,6 +1334,28 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     e1 = nullptr;
   }
   hipError_t err = hipSuccess;
+  if (is_qsgd(in_dtype)) {
+    // quantised records: one tile per workgroup, exact client order (no split, no persistent
+    // grid); the record layout needs 16-B aligned records; outputs may be unaligned
+    if (st.delta) return fail(FEDAVG_ERR_INVALID, "quantised records cannot be delta updates");
+    if (!st.clients_aligned) return fail(FEDAVG_ERR_INVALID, "quantised records must be 16-byte aligned");
+    a.tiles = c->d_tiles1;
+    a.tile_begin = tb_split1;
+    a.num_tiles = te_split1 - tb_split1;
+    if (a.num_tiles <= 0) return FEDAVG_OK;
+    switch (out_kind) {
+      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1); break;
+      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1); break;
+      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1); break;
+      default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
+    }
+    if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
+    if (m1) {
+      FEDAVG_HIP_TRY(hipEventRecord(m1, s));
+      if (done_ev) *done_ev = m1;
+    }
+    return FEDAVG_OK;
+  }
   const int fold = st.delta ? FOLD_DELTA
                             : (c->allow_fma && fma_exact_call(st, in_dtype)) ? FOLD_FMA : FOLD_MULADD;
   switch (out_kind) {
@@ -1151,6 +1417,16 @@ int out_kind_of(int32_t out_dtype) {
 extern "C" {
 
 int32_t fedavg_abi_version(void) { return FEDAVG_ABI_VERSION; }
+
+int64_t fedavg_qsgd_sign_offset(int64_t numel) {
+  if (numel < 0) return -1;
+  return 16 + static_cast<int64_t>(align_up(static_cast<size_t>(numel), 16));
+}
+
+int64_t fedavg_qsgd_record_bytes(int64_t numel) {
+  if (numel < 0) return -1;
+  return fedavg_qsgd_sign_offset(numel) + static_cast<int64_t>(align_up(static_cast<size_t>((numel + 7) / 8), 16));
+}
 
 const char* fedavg_last_error(void) { return g_last_error.c_str(); }
 
@@ -1557,6 +1833,8 @@ int32_t fedavg_find_nan_clients(fedavg_ctx* c, const void* const* client_ptrs, i
     dim3 grid(static_cast<unsigned>(c->tiles1.size()), static_cast<unsigned>(K));
     const void* const* tab = static_cast<const void* const*>(d_tab);
     switch (in_dtype) {
+      case FEDAVG_QSGD_F32: hipLaunchKernelGGL(qsgd_nan_scan_kernel<float>, grid, dim3(kThreads), 0, s, c->d_tiles1, c->d_segs, tab, K, d_bad); break;
+      case FEDAVG_QSGD_F64: hipLaunchKernelGGL(qsgd_nan_scan_kernel<double>, grid, dim3(kThreads), 0, s, c->d_tiles1, c->d_segs, tab, K, d_bad); break;
       case FEDAVG_F32: hipLaunchKernelGGL(nan_scan_kernel<float>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
       case FEDAVG_F16: hipLaunchKernelGGL(nan_scan_kernel<__half>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
       case FEDAVG_BF16: hipLaunchKernelGGL(nan_scan_kernel<bf16_t>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;

@@ -92,7 +92,14 @@ def _stream_handle(device: torch.device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def dtype_code(dtype: torch.dtype) -> int:
+def dtype_code(dtype) -> int:
+    """C-ABI input format of a torch dtype, or of a quantised record format
+    (``quantized.QSGD_F32`` / ``QSGD_F64``, which carry their own code)."""
+    if not isinstance(dtype, torch.dtype):
+        code = getattr(dtype, "code", None)
+        if code in (_native.QSGD_F32, _native.QSGD_F64):
+            return int(code)
+        raise TypeError(f"no HIP FedAvg kernel for input format {dtype}")
     try:
         return DTYPE_CODES[dtype]
     except KeyError:

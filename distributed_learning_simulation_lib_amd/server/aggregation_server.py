@@ -27,6 +27,7 @@ from typing import Any
 import torch
 
 from ..message import DeltaParameterMessage, Message, ParameterMessage, ParameterMessageBase
+from ..quantized import dequantize_parameter, is_quantized
 
 
 class ModelCache:
@@ -130,6 +131,7 @@ class AggregationServer:
                 if not isinstance(data, ParameterMessageBase):
                     return
             old_parameter = self._model_cache.parameter
+            self._dequantize_if_needed(data)
             if isinstance(data, DeltaParameterMessage):
                 assert old_parameter is not None
                 if getattr(self._algorithm, "accepts_delta_messages", False):
@@ -147,6 +149,18 @@ class AggregationServer:
             result = self._aggregate_worker_data()
             self._send_result(result)
             self._worker_flag.clear()
+
+    def _dequantize_if_needed(self, data: Message) -> None:
+        """QuantServerEndpoint.get (topology/quantized_endpoint.py:69-77): quantised payloads
+        are dequantised before the algorithm sees them — unless the algorithm folds QSGD
+        records itself (FedAVGAlgorithm: dequantisation fused into the kernel). Deltas are
+        always dequantised (the delta fold takes dense tensors)."""
+        if isinstance(data, DeltaParameterMessage):
+            if is_quantized(data.delta_parameter):
+                data.delta_parameter = dequantize_parameter(data.delta_parameter)
+        elif isinstance(data, ParameterMessage) and is_quantized(data.parameter):
+            if not getattr(self._algorithm, "accepts_quantized_messages", False):
+                data.parameter = dequantize_parameter(data.parameter)
 
     def _aggregate_worker_data(self) -> Message:
         self._algorithm.set_old_parameter(self._model_cache.parameter)

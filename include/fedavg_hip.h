@@ -56,6 +56,21 @@ enum fedavg_dtype {
   FEDAVG_F16 = 1,
   FEDAVG_BF16 = 2,
   FEDAVG_F64 = 3,
+  /* Quantised client records (server-side dequantisation fused into the fold,
+   * StochasticQuantServerEndpoint.get, simulation_lib/topology/quantized_endpoint.py:69-77 and
+   * :102-111). A client "tensor" pointer then points at one QSGD record of the tensor
+   * (16-byte aligned, fedavg_qsgd_record_bytes(numel) bytes):
+   *   [0, 8)   norm, fp64 (for FEDAVG_QSGD_F32 an fp32 value held exactly)
+   *   [8, 12)  quantisation level s, int32 in [1, 255] (the reference uses 255)
+   *   [16, 16 + numel)             slot per element, uint8 in [0, s]
+   *   [fedavg_qsgd_sign_offset(numel), + ceil(numel / 8))  sign bits in numpy.packbits order
+   *            (element i: byte i / 8, bit 7 - i % 8; 1 = non-negative)
+   * The dequantised element is x = ((norm * sign) * slot) / s computed in fp32 (QSGD_F32) or
+   * fp64 (QSGD_F64) — the codec's dtype — and is then folded exactly like a dense input
+   * (tmp = x.to(f64) * w; acc += tmp). Accepted by every fold entry point except the delta
+   * ones; split policies do not apply. */
+  FEDAVG_QSGD_F32 = 4,
+  FEDAVG_QSGD_F64 = 5,
 };
 
 /* status codes */
@@ -78,6 +93,11 @@ enum fedavg_status {
 typedef struct fedavg_ctx fedavg_ctx;
 
 int32_t fedavg_abi_version(void);
+
+/* Byte size of one QSGD record of a numel-element tensor, and the offset of its sign bits
+ * (see FEDAVG_QSGD_F32). Pure functions; -1 for numel < 0. */
+int64_t fedavg_qsgd_record_bytes(int64_t numel);
+int64_t fedavg_qsgd_sign_offset(int64_t numel);
 const char* fedavg_last_error(void);
 
 /*

@@ -344,30 +344,22 @@ def main_personalized(args: argparse.Namespace) -> int:
 
 
 def make_qsgd_clients(layout: ModelLayout, n: int, device: torch.device, level: int = 255):
-    """n synthetic QSGD-quantised clients (fp32 codec), records resident in HBM: slots uniform in
-    [0, level], random sign bits, per-tensor norms |N(0,1)| — the byte stream a
-    StochasticQuantClientEndpoint worker sends (quantized_endpoint.py:96-99)."""
-    from distributed_learning_simulation_lib_amd.quantized import record_bytes, sign_offset
+    """n synthetic QSGD-quantised clients (fp32 codec), records resident in HBM: each client's
+    x ~ N(0,1) (seeded per client) quantised with the client-side quantiser
+    (quantized.quantize_tensor, level 255) — the byte stream a StochasticQuantClientEndpoint
+    worker sends (quantized_endpoint.py:96-99)."""
+    from distributed_learning_simulation_lib_amd.quantized import quantize_tensor, record_bytes
 
     sizes = [record_bytes(m) for m in layout.numels]
     offs = np.cumsum([0] + sizes[:-1]).tolist()
     total = sum(sizes)
     buckets = torch.zeros((n, total), dtype=torch.uint8, device=device)
     g = torch.Generator(device=device)
-    hdr = torch.zeros(16, dtype=torch.uint8)
-    hdr[8:12] = torch.tensor([level], dtype=torch.int32).view(torch.uint8)
-    rng = np.random.default_rng(7)
     for i in range(n):
-        g.manual_seed(4321 + i)
-        for o, m in zip(offs, layout.numels):
-            rec = buckets[i, o : o + record_bytes(m)]
-            h = hdr.clone()
-            h[0:8] = torch.tensor([abs(float(rng.standard_normal())) + 0.1], dtype=torch.float64).view(torch.uint8)
-            rec[0:16] = h.to(device)
-            rec[16 : 16 + m] = torch.randint(0, level + 1, (m,), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
-            so = sign_offset(m)
-            nb = (m + 7) // 8
-            rec[so : so + nb] = torch.randint(0, 256, (nb,), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
+        g.manual_seed(1234 + i)
+        for o, m, sz in zip(offs, layout.numels, sizes):
+            x = torch.randn(m, generator=g, device=device)
+            buckets[i, o : o + sz] = quantize_tensor(x, level, generator=g).record
     views = [[buckets[i, o : o + sz] for o, sz in zip(offs, sizes)] for i in range(n)]
     return buckets, views, total
 
@@ -485,7 +477,7 @@ def main_qsgd(args: argparse.Namespace) -> int:
         "vs_baseline": None,
         "client_elements_per_s": round(N * P / step_s, 1),
         "dtype": "f64",
-        "data": "synthetic QSGD records: slots uniform in [0, 255], random signs, norms |N(0,1)|+0.1; dataset-size weights",
+        "data": "synthetic: x ~ N(0,1) per client, QSGD-quantised on the GPU (inf-norm, level 255, stochastic rounding); dataset-size weights",
         "config": {"workload": f"fedavg_qsgd255_{args.layout}_{N}_clients", "clients": N, "params_per_client": P,
                    "tensors_per_client": T, "record_bytes_per_client": client_bytes, "codec": "qsgd_f32 (level 255)",
                    "accumulate_dtype": "float64", "out_dtype": args.out_dtype},

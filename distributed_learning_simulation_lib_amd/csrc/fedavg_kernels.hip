@@ -699,7 +699,16 @@ __global__ __launch_bounds__((Geo<T, SPLIT>::THREADS), FEDAVG_MIN_WAVES) void fe
 // [16 li, 16 li + 16) (one 16-B slot load + one 2-B sign load per client; a wave reads 1 KiB of
 // slots contiguously). Clients go in groups of QG: the group's loads are issued, its QG tables
 // are built into one of two LDS buffers, one barrier, then the fold in arrival order.
-constexpr int kQsgdGroup = 4;
+#ifndef FEDAVG_QSGD_READ_FENCE
+#define FEDAVG_QSGD_READ_FENCE 1
+#endif
+#ifndef FEDAVG_QSGD_ABLATE
+#define FEDAVG_QSGD_ABLATE 0
+#endif
+#ifndef FEDAVG_QSGD_GROUP
+#define FEDAVG_QSGD_GROUP 4
+#endif
+constexpr int kQsgdGroup = FEDAVG_QSGD_GROUP;
 constexpr int kQsgdLanes = 256;
 constexpr int kQsgdAE = 16;
 
@@ -750,56 +759,106 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
     have = true;
   }
 
-  int buf = 0;
-  for (int k = 0; k < kseg; k += kQsgdGroup) {
-    const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
+  // Client loads of one group (slots + sign words), issued one group ahead of its fold so the
+  // HBM latency of group g+1 hides under the table build and fold of group g.
+  struct GroupRegs {
     u32x4 slots[kQsgdGroup];
     uint32_t signs[kQsgdGroup];
-    double nrm[kQsgdGroup], wk[kQsgdGroup];
+    double nrm[kQsgdGroup], wk[kQsgdGroup];  // wave-uniform (SGPRs): record header, weight
     int lvl[kQsgdGroup];
+  };
+  auto issue = [&](GroupRegs& r, int k) {
+    const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
 #pragma unroll
     for (int c = 0; c < kQsgdGroup; ++c) {
       const int kc = k + min(c, n - 1);
       const uint64_t rec = cp[kc];
-      const kptr<double> hdr = to_const<double>(reinterpret_cast<const void*>(rec));
-      nrm[c] = hdr[0];
-      lvl[c] = to_const<int32_t>(reinterpret_cast<const void*>(rec))[2];
-      wk[c] = wp[kc];
+      r.nrm[c] = to_const<double>(reinterpret_cast<const void*>(rec))[0];
+      r.lvl[c] = to_const<int32_t>(reinterpret_cast<const void*>(rec))[2];
+      r.wk[c] = wp[kc];
       if (lane_live) {
-        const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(rec));
+        const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(cp[kc]));
 #if FEDAVG_NT
-        slots[c] = __builtin_nontemporal_load((gptr<const u32x4>)(rp + slot_off));
+        r.slots[c] = __builtin_nontemporal_load((gptr<const u32x4>)(rp + slot_off));
 #else
-        slots[c] = *(gptr<const u32x4>)(rp + slot_off);
+        r.slots[c] = *(gptr<const u32x4>)(rp + slot_off);
 #endif
-        signs[c] = *(gptr<const uint16_t>)(rp + sign_off);
+        r.signs[c] = *(gptr<const uint16_t>)(rp + sign_off);
       } else {
-        slots[c] = u32x4{0u, 0u, 0u, 0u};
-        signs[c] = 0xffffu;
+        r.slots[c] = u32x4{0u, 0u, 0u, 0u};
+        r.signs[c] = 0xffffu;
       }
     }
-    // this group's product tables: lane li tabulates slot value li of every client
+  };
+  // Table build + fold of one group into LDS buffer B (compile-time, so every table read is
+  // `ds_read_b64 v, v_off offset:<buffer base>`). The table holds |p|; the sign of each
+  // product is sign(x_hat) ^ sign(w) = (element negative) ^ signbit(norm) ^ signbit(w)
+  // (every step of the dequantisation and the product is sign-symmetric, zeros included),
+  // inserted into the high word with one bit-field insert.
+  auto run = [&](auto buf_tag, const GroupRegs& r, int k) {
+    constexpr int B = decltype(buf_tag)::value;
+    const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
+    uint32_t neg[kQsgdGroup];  // per element: 1 = the product is negative (bit layout of signs)
 #pragma unroll
-    for (int c = 0; c < kQsgdGroup; ++c) lut[buf][c][li] = qsgd_product<DQ>(nrm[c], lvl[c], li, wk[c]);
+    for (int c = 0; c < kQsgdGroup; ++c) {
+      const double nrm = r.nrm[c], wk = r.wk[c];
+      // this group's product tables: lane li tabulates slot value li of every client
+#if FEDAVG_QSGD_ABLATE == 2  // timing only: no table build (wrong results)
+      lut[B][c][li] = nrm * wk;
+#else
+      lut[B][c][li] = __builtin_fabs(qsgd_product<DQ>(nrm, r.lvl[c], li, wk));
+#endif
+      const bool flip = __builtin_signbit(nrm) != __builtin_signbit(wk);  // wave-uniform
+      neg[c] = flip ? r.signs[c] : ~r.signs[c];
+    }
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < kQsgdGroup; ++c) {
       if (c < n) {
-        const double* tab = lut[buf][c];
-        // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte,
-        // element j >= 8 bit 15 - (j - 8) of the high byte of the little-endian 16-bit word
+        const char* tab = reinterpret_cast<const char*>(lut[B][c]);
+        // all 16 table reads of this client in flight before the first add (the compiler
+        // otherwise keeps ~4 outstanding and waits on each batch)
+        double pav[AE];
 #pragma unroll
         for (int j = 0; j < AE; ++j) {
-          const uint32_t word = slots[c][j >> 2];
-          const uint32_t s = (word >> (8 * (j & 3))) & 0xffu;
+          const uint32_t word = r.slots[c][j >> 2];
+          const uint32_t off = ((word >> (8 * (j & 3))) & 0xffu) << 3;
+#if FEDAVG_QSGD_ABLATE == 1  // timing only: no table reads (wrong results)
+          pav[j] = static_cast<double>(off);
+#else
+          pav[j] = *reinterpret_cast<const double*>(tab + off);
+#endif
+        }
+#if FEDAVG_QSGD_READ_FENCE
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+        for (int j = 0; j < AE; ++j) {
+          // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte of
+          // the little-endian 16-bit sign word, element j >= 8 bit 15 - (j - 8)
           const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
-          const bool pos = (signs[c] >> bit) & 1u;
-          const double p = tab[s];
-          acc[j] = acc[j] + (pos ? p : -p);
+          const uint32_t sb = neg[c] << (31 - bit);
+          const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pav[j]));
+          const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
+          const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
+          acc[j] = acc[j] + p;
         }
       }
     }
-    buf ^= 1;  // the next group writes the other buffer; the barrier above orders the reuse
+  };
+  // Two groups per iteration (LDS buffers 0 / 1): the next group's tables go into the other
+  // buffer, and the barrier before its fold orders the reuse (every lane has finished the fold
+  // two groups back). Loads run one group ahead.
+  GroupRegs r0, r1;
+  if (kseg > 0) issue(r0, 0);
+  for (int k = 0; k < kseg; k += 2 * kQsgdGroup) {
+    const bool second = k + kQsgdGroup < kseg;
+    if (second) issue(r1, k + kQsgdGroup);
+    run(std::integral_constant<int, 0>{}, r0, k);
+    if (second) {
+      if (k + 2 * kQsgdGroup < kseg) issue(r0, k + 2 * kQsgdGroup);
+      run(std::integral_constant<int, 1>{}, r1, k + kQsgdGroup);
+    }
   }
   have = have || (kseg > 0);
   if (!have) return;

@@ -709,6 +709,7 @@ __global__ __launch_bounds__((Geo<T, SPLIT>::THREADS), FEDAVG_MIN_WAVES) void fe
 #define FEDAVG_QSGD_GROUP 4
 #endif
 constexpr int kQsgdGroup = FEDAVG_QSGD_GROUP;
+constexpr int kQsgdTable = 256;  // entries per client (|p| per slot value)
 constexpr int kQsgdLanes = 256;
 constexpr int kQsgdAE = 16;
 
@@ -723,7 +724,7 @@ __device__ __forceinline__ double qsgd_product(double norm, int level, int slot,
 }
 
 template <int OUT, typename DQ, bool FULL, bool VEC>
-__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][256]) {
+__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable]) {
   constexpr int AE = kQsgdAE;
   const int seg = td.seg;
   const int count = td.count;
@@ -925,7 +926,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
 
 template <int OUT, typename DQ, bool VEC>
 __global__ __launch_bounds__(kQsgdLanes) void qsgd_tile_kernel(KArgs a) {
-  __shared__ double lut[2][kQsgdGroup][256];
+  __shared__ double lut[2][kQsgdGroup][kQsgdTable];
   const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
   if (td.count == kTile1) {
     qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut);

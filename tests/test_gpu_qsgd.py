@@ -206,3 +206,51 @@ def test_plugin_with_quantised_messages(hip_device, from_host, accumulate):
     for name, s in shapes.items():
         assert tuple(res[name].shape) == s
         assert bits_equal(res[name].reshape(-1).cpu().numpy(), want[name])
+
+
+# ---- property test: random quantised rounds through the plugin ------------------------------
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+from oracle.fedavg_oracle import OracleFedAvg, OracleMessage  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(n=st.integers(1, 20), sizes=st.lists(st.integers(1, 9000), min_size=1, max_size=4),
+       codec=st.sampled_from(["float32", "float64"]), level=st.sampled_from([1, 7, 100, 255]),
+       int_weights=st.booleans(), wave=st.integers(1, 25), seed=st.integers(0, 2**31 - 1),
+       skip_every=st.integers(0, 4), neg_weight=st.booleans())
+def test_random_quantised_rounds_bit_identical(hip_device, n, sizes, codec, level, int_weights, wave, seed,
+                                               skip_every, neg_weight):
+    """Random layouts / client counts / levels / wave sizes / skipped clients / weight signs:
+    the plugin's fused fold equals the oracle dequantisation + the pinned FedAvg oracle."""
+    rng = np.random.default_rng(seed)
+    weights = ([float(x) for x in rng.integers(1, 5000, size=n)] if int_weights
+               else [float(x) for x in rng.uniform(1e-3, 10.0, size=n)])
+    if neg_weight and n > 1:
+        weights[1] = -weights[1] * 0.25  # a negative weight flips the product signs (table sign logic)
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=wave, result_dtype=torch.float64)
+    oracle = OracleFedAvg()
+    for k in range(n):
+        if skip_every and k % skip_every == skip_every - 1 and k != 0:
+            algo.process_worker_data(k, None)
+            oracle.process_worker_data(k, None)
+            continue
+        params, dense = {}, {}
+        for i, s in enumerate(sizes):
+            x = (rng.standard_normal(s) * rng.choice([1e-30, 1e-3, 1.0, 1e30])).astype(codec)
+            rec = qo.quantize(x, rng, level=level)
+            params[f"t{i}"] = QuantizedTensor(torch.from_numpy(rec).to(hip_device), (s,), CODECS[codec])
+            dense[f"t{i}"] = qo.dequantize(rec, s, codec)
+        algo.process_worker_data(k, ParameterMessage(parameter=params, aggregation_weight=weights[k]))
+        oracle.process_worker_data(k, OracleMessage(parameter=dense, aggregation_weight=weights[k]))
+    try:
+        want = oracle.aggregate_worker_data().parameter
+    except AssertionError:
+        with pytest.raises(AssertionError):
+            algo.aggregate_worker_data()
+        return
+    got = algo.aggregate_worker_data().parameter
+    for name, w in want.items():
+        assert bits_equal(got[name].reshape(-1).cpu().numpy(), w.reshape(-1)), name

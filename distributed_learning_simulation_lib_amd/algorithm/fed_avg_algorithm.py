@@ -75,6 +75,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__has_data = False
         self.__ingest: HostIngest | None = None
         self.__result_flat: torch.Tensor | None = None
+        self.__record_layouts: dict[tuple[int, ...], ModelLayout] = {}
 
     # ---- setup -------------------------------------------------------------------------
     @property
@@ -267,9 +268,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if host:
             if self.__ingest is None:
                 self.__ingest = HostIngest(self.device)
-            numels = [q.numel if q is not None else 1 for q in tensors]
+            numels = tuple(q.numel if q is not None else 1 for q in tensors)
+            rl = self.__record_layouts.get(numels)
+            if rl is None:
+                rl = self.__record_layouts[numels] = record_layout(list(numels))
             staged = self.__ingest.to_device(
-                record_layout(numels),
+                rl,
                 [q.record if q is not None and q.device.type == "cpu" else None for q in tensors],
                 torch.uint8,
             )
@@ -330,7 +334,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         flat = self.__result_flat
         if self.result_device.type != "cpu" or flat is None:
             return {k: v.to(self.result_device) for k, v in out.items()}
-        host = flat.to(self.result_device)
+        # through torch's caching pinned-host allocator: a DMA at full PCIe rate instead of a
+        # pageable copy (the pinned block is reused once the previous round's result is freed)
+        host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+        host.copy_(flat)
         moved: ModelParameter = {}
         for name, v in out.items():
             if v.numel() and v.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr():

@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes
 from collections.abc import Mapping, Sequence
 from dataclasses import dataclass
+from functools import cached_property
 
 import numpy as np
 import torch
@@ -66,8 +67,9 @@ class ModelLayout:
     def flat(cls, numel: int, name: str = "bucket") -> ModelLayout:
         return cls(names=(name,), shapes=((int(numel),),))
 
-    @property
+    @cached_property
     def numels(self) -> list[int]:
+        # cached: the staging path asks for it per client (np.prod per tensor is ~2 us)
         return [int(np.prod(s, dtype=np.int64)) for s in self.shapes]
 
     @property
@@ -80,6 +82,13 @@ class ModelLayout:
 
     def padded_offsets(self, elem_bytes: int) -> tuple[list[int], int]:
         """Element offsets of each tensor in a flat buffer whose segments start 16-B aligned."""
+        cache = self.__dict__.setdefault("_padded_cache", {})
+        if elem_bytes not in cache:
+            cache[elem_bytes] = self._padded_offsets(elem_bytes)
+        offs, total = cache[elem_bytes]
+        return list(offs), total
+
+    def _padded_offsets(self, elem_bytes: int) -> tuple[list[int], int]:
         align = max(1, 16 // elem_bytes)
         offs, pos = [], 0
         for n in self.numels:

@@ -10,6 +10,8 @@ ResNet-18 layout:
                          aggregate_worker_data, result copied to the host as float64 (what the
                          reference server caches, util/model_cache.py:27-34)
   plugin_pageable_fp64 : the same with float64 payloads (what AggregationWorker sends)
+  plugin_pageable_qsgd255: the same with QSGD-quantised payloads (level 255; records staged
+                         through the pinned ingest, dequantised inside the fold)
   pinned_pipelined_fp32: payloads in pinned host buckets; H2D copies on a copy stream, one
                          accumulate launch per wave of 8 clients as soon as its copies land,
                          fp64 result D2H
@@ -80,6 +82,27 @@ for dtype, name in ((torch.float32, "plugin_pageable_fp32"), (torch.float64, "pl
     nbytes = K * P * clients[0][0].element_size() + P * 8
     results[name] = {"round_ms": round(min(times) * 1e3, 2), "GBps": round(nbytes / min(times) / 1e9, 2)}
     del clients
+
+# QSGD-quantised updates in host memory (StochasticQuantServerEndpoint): the plugin stages the
+# records (1.125 B/element) through the pinned ingest and the kernel dequantises in the fold
+from distributed_learning_simulation_lib_amd.quantized import quantize_tensor  # noqa: E402
+
+dense = host_clients(torch.float32, pinned=False)
+qclients = []
+gq = torch.Generator(device=dev).manual_seed(11)
+for flat, d in dense:
+    qd = {n: quantize_tensor(t.to(dev), generator=gq).to("cpu") for n, t in d.items()}
+    qclients.append((None, qd))
+del dense
+plugin_round(qclients)  # warm
+times = [plugin_round(qclients) for _ in range(3)]
+rec_bytes = sum(q.record.numel() for q in qclients[0][1].values())
+results["plugin_pageable_qsgd255"] = {
+    "round_ms": round(min(times) * 1e3, 2),
+    "GBps": round((K * rec_bytes + P * 8) / min(times) / 1e9, 2),
+    "fp32_equivalent_GBps": round((K * P * 4 + P * 8) / min(times) / 1e9, 2),
+}
+del qclients
 
 # pinned, pipelined H2D (copy stream) + per-wave accumulate on the compute stream
 clients = host_clients(torch.float32, pinned=True)

@@ -81,3 +81,35 @@ def test_native_comm_rejects_bad_arguments(hip_device, nccl_group):
     assert lib.fedavg_sharded_round(comm.handle, ctx._h, plan._h, None, 1, 5, None) == _native.ERR_INVALID
     assert lib.fedavg_sharded_round(comm.handle, ctx._h, plan._h, None, 1, 0, None) == _native.ERR_INVALID
     comm.close()
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_forced_collective_with_quantised_records(native, hip_device, nccl_group):
+    """The sharded round over QSGD records (dequantisation fused into the shard partials) equals
+    the fused single-launch quantised aggregate bit for bit on a one-rank world."""
+    from distributed_learning_simulation_lib_amd.quantized import QSGD_F32, quantize_tensor
+
+    layout = ModelLayout(names=("a", "b"), shapes=((50001,), (4096 * 3,)))
+    g = torch.Generator(device=hip_device).manual_seed(3)
+    table = ClientTable(2)
+    weights = [float(w) for w in np.random.default_rng(4).integers(100, 5000, size=9)]
+    for w in weights:
+        recs = [quantize_tensor(torch.randn(n, device=hip_device, generator=g), generator=g).record
+                for n in layout.numels]
+        table.add_client(recs, [w] * 2)
+    totals = [sum(weights)] * 2
+    ctx_a = FedAvgContext(layout, hip_device)
+    out_a = [torch.empty(n, dtype=torch.float32, device=hip_device) for n in layout.numels]
+    ctx_a.aggregate(table, QSGD_F32, out_a, torch.float32)
+    ctx_a.raise_on_nan()
+    ctx_b = FedAvgContext(layout, hip_device)
+    out_b = [torch.empty(n, dtype=torch.float32, device=hip_device) for n in layout.numels]
+    comm = RcclComm(hip_device) if native else None
+    red = HipLocalReducer(ctx_b, table, QSGD_F32, out_b, torch.float32)
+    sharded_reduce(red, totals, chunks=3, force_collective=True, comm=comm)
+    ctx_b.raise_on_nan()
+    for a, b in zip(out_a, out_b):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    if comm is not None:
+        torch.cuda.synchronize(hip_device)
+        comm.close()

@@ -731,6 +731,8 @@ def main() -> int:
             "mean_launch_ms": round(per_launch_ms, 4),
             "launches": launches,
         },
+        # the input-only form N·P·s_in / t beside the algorithmic-bytes value
+        "input_only_GBps": round(n_total * P * in_bytes / step_s / 1e9, 2),
         "host_enqueue_ms_per_step": round(host_enqueue[0] * 1e3 / args.steps, 4),
         "hbm_probe": probe,
         "cpu_baseline": cpu,

@@ -78,14 +78,19 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_AE_HALF  // elements per lane for 2-byte inputs (fp16 / bf16)
 #define FEDAVG_AE_HALF 8
 #endif
-#ifndef FEDAVG_AE_F64  // elements per lane for fp64 inputs
-#define FEDAVG_AE_F64 16
+#ifndef FEDAVG_AE_F64  // elements per lane for fp64 inputs (8: 512-lane tiles, see CU_BYTES_F64)
+#define FEDAVG_AE_F64 8
 #endif
 #ifndef FEDAVG_TILE1  // elements per tile of the exact-order kernel (all dtypes)
 #define FEDAVG_TILE1 4096
 #endif
 #ifndef FEDAVG_CU_BYTES
 #define FEDAVG_CU_BYTES 256
+#endif
+#ifndef FEDAVG_CU_BYTES_F64  // the same for fp64 inputs: 8 clients x 64 B in flight per lane
+// (64 x ResNet-18 fp64, interleaved A/B: AE 8 / 512 B 0.898-0.915 ms vs AE 16 / 256 B
+// 0.974-0.984 ms; AE 8 / 768 B, AE 4, AE 32 and AE 16 / 512 B no better than the old default)
+#define FEDAVG_CU_BYTES_F64 512
 #endif
 #ifndef FEDAVG_NT
 #define FEDAVG_NT 1
@@ -392,7 +397,8 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   constexpr int N = LL::N;
   constexpr int VPL = LL::VPL;
   // clients in flight per lane: 256 B of loads per lane per group
-  constexpr int CU_LOADS = (FEDAVG_CU_BYTES / (VPL * 16)) < 2 ? 2 : (FEDAVG_CU_BYTES / (VPL * 16));
+  constexpr int CU_B = sizeof(T) == 8 ? FEDAVG_CU_BYTES_F64 : FEDAVG_CU_BYTES;
+  constexpr int CU_LOADS = (CU_B / (VPL * 16)) < 2 ? 2 : (CU_B / (VPL * 16));
   constexpr bool FAST = FULL && VEC;
 
   const int seg = td.seg;

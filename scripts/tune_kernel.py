@@ -13,9 +13,9 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "h16": {"FEDAVG_AE_HALF": 16},
-    "h16_cu512": {"FEDAVG_AE_HALF": 16, "FEDAVG_CU_BYTES": 512},
-    "h8_cu128": {"FEDAVG_CU_BYTES": 128},
+    "cu512": {"FEDAVG_CU_BYTES": 512},
+    "cu384": {"FEDAVG_CU_BYTES": 384},
+    "f8_cu512": {"FEDAVG_AE": 8, "FEDAVG_CU_BYTES": 512},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

@@ -13,9 +13,8 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "cu512": {"FEDAVG_CU_BYTES": 512},
-    "cu384": {"FEDAVG_CU_BYTES": 384},
-    "f8_cu512": {"FEDAVG_AE": 8, "FEDAVG_CU_BYTES": 512},
+    "w4": {"FEDAVG_MIN_WAVES": 4},
+    "w2": {"FEDAVG_MIN_WAVES": 2},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

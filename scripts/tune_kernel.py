@@ -13,8 +13,7 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "w4": {"FEDAVG_MIN_WAVES": 4},
-    "w2": {"FEDAVG_MIN_WAVES": 2},
+    "t8k": {"FEDAVG_TILE1": 8192},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

@@ -665,6 +665,27 @@ def main() -> int:
         achieved = rank_bytes / (per_launch_ms * 1e-3) / 1e9 if launches else 0.0
         kernel_desc = f"fedavg_tile_kernel<{kname}, OUT_ACC, 1, true, fma> (partial, first of {args.chunks} chunks)"
 
+    # Diagnostic for the sharded round (untimed, after the timed region): the same number of
+    # partial-only rounds (the chunk kernels without the exchange), so the line shows how much
+    # of the step is the exposed reduce tail + the root's finalize.
+    partial_only_ms = None
+    pplan = getattr(reducer, "_partial_plan", None) if sharded else None
+    if pplan is not None:
+        torch.cuda.synchronize(device)
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        p0 = time.perf_counter()
+        for _ in range(args.steps):
+            pplan.run()
+        torch.cuda.synchronize(device)
+        p_el = time.perf_counter() - p0
+        if dist.is_initialized():
+            pt = torch.tensor([p_el], dtype=torch.float64, device=device)
+            dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+            p_el = float(pt.item())
+        partial_only_ms = p_el / args.steps * 1e3
+
     traffic, traffic_src = (None, None)
     if not sharded and n_waves == 1 and args.layout == "resnet18":
         traffic, traffic_src = committed_traffic(world, n_local, args.in_dtype, args.out_dtype)
@@ -711,7 +732,12 @@ def main() -> int:
             "accumulate_dtype": "float64",
             "out_dtype": args.out_dtype,
             "parallelism": "single GPU" if world == 1 else f"clients sharded over {world} GPUs + chunked RCCL reduce to rank 0",
-            "exchange": None if not sharded else {"chunks": args.chunks, "comm": args.comm},
+            "exchange": None if not sharded else {
+                "chunks": args.chunks, "comm": args.comm,
+                "partial_only_ms_per_step": None if partial_only_ms is None else round(partial_only_ms, 4),
+                "exposed_exchange_and_finalize_ms": (None if partial_only_ms is None
+                                                     else round(step_s * 1e3 - partial_only_ms, 4)),
+            },
             "baseline_config": ("BASELINE.json configs[1]" if (world == 1 and args.layout == "resnet18" and n_local == 64)
                                 else "BASELINE.json configs[2] (weak-scaled, 64 clients/GPU)" if args.layout == "resnet18"
                                 else "see DESIGN.md"),

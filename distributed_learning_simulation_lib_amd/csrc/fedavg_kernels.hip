@@ -112,6 +112,10 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #endif
 constexpr int kAE = FEDAVG_AE;    // elements owned by one lane (fp64 accumulators per lane)
 constexpr int kTile1 = FEDAVG_TILE1;          // 4096 elements, SPLIT = 1 (any dtype)
+#ifndef FEDAVG_TILE_WIDE  // whole-layout exact-order launches of 2- and 4-byte inputs (0 = off)
+#define FEDAVG_TILE_WIDE 8192
+#endif
+constexpr int kTileWide = FEDAVG_TILE_WIDE;
 constexpr int kTile4 = (kThreads / 4) * kAE;  // 1024 elements, SPLIT = 4
 
 struct TileDesc {
@@ -334,15 +338,23 @@ struct LaneLoader {
 // slice: 16 elements (fp32 / fp64: a client's tile slice is 16 KiB resp. 32 KiB contiguous,
 // 4 / 2 clients in flight per group) or 8 (fp16 / bf16: 512-lane workgroups, 16 clients per
 // group) — the fastest shapes measured on MI355X. The split kernel keeps kAE for all dtypes.
-template <typename T, int SPLIT>
+//
+// Whole-layout launches of 2- and 4-byte inputs (no tile range: one-shot aggregates, waves,
+// full partials) use a second table of kTileWide = 8192-element tiles (TILEN = kTileWide:
+// 512 / 1024-lane workgroups, 32 / 16 KiB contiguous per client per tile): +1.3 % (fp32) and
+// +3 % (fp16) on 64 x ResNet-18, interleaved A/B. Any partition of the elements gives the same
+// per-element fold, so both tables produce identical bits; ranged launches (sharded chunks,
+// finalize ranges) keep the 4096-element table their tile indices refer to. fp64 keeps 4096
+// (1024-lane tiles measured -15 %).
+template <typename T, int SPLIT, int TILEN = kTile1>
 struct Geo {
   static constexpr int AE = (SPLIT > 1) ? kAE
                           : (sizeof(T) == 2 ? FEDAVG_AE_HALF : sizeof(T) == 8 ? FEDAVG_AE_F64 : kAE);
-  static constexpr int LANES = (SPLIT > 1) ? 64 : kTile1 / AE;
+  static constexpr int LANES = (SPLIT > 1) ? 64 : TILEN / AE;
   static constexpr int THREADS = (SPLIT > 1) ? kThreads : LANES;
   static constexpr int TILE = LANES * AE;
   static_assert(SPLIT == 1 || TILE == kTile4, "split tiles");
-  static_assert(SPLIT > 1 || TILE == kTile1, "tile geometry");
+  static_assert(SPLIT > 1 || TILE == TILEN, "tile geometry");
   static_assert(THREADS % 64 == 0 && THREADS <= 1024, "workgroup size");
 };
 
@@ -388,10 +400,10 @@ __device__ __forceinline__ double fold(double acc, double x, double w, double ba
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD>
+template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD, int TILEN = kTile1>
 __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
-  constexpr int AE = Geo<T, SPLIT>::AE;
-  constexpr int LANES = Geo<T, SPLIT>::LANES;  // lanes sharing one client stream
+  constexpr int AE = Geo<T, SPLIT, TILEN>::AE;
+  constexpr int LANES = Geo<T, SPLIT, TILEN>::LANES;  // lanes sharing one client stream
   using LL = LaneLoader<T, LANES, FULL && VEC, VEC, AE>;
   using V = typename LL::V;
   constexpr int N = LL::N;
@@ -657,10 +669,10 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC, int FOLD>
-__global__ __launch_bounds__((Geo<T, SPLIT>::THREADS), FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
+template <typename T, int OUT, int SPLIT, bool VEC, int FOLD, int TILEN = kTile1>
+__global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
-  constexpr int TILE = Geo<T, SPLIT>::TILE;
+  constexpr int TILE = Geo<T, SPLIT, TILEN>::TILE;
   // Persistent form (exact-order kernel): a grid of (resident blocks) workgroups walks the
   // tiles with stride gridDim.x, so the tiles in flight at any moment are one contiguous range
   // of every client bucket and no block is launched per tile. The split kernel keeps one
@@ -669,9 +681,9 @@ __global__ __launch_bounds__((Geo<T, SPLIT>::THREADS), FEDAVG_MIN_WAVES) void fe
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const TileDesc td = load_tile(a.tiles, a.tile_begin + t);
     if (td.count == TILE) {
-      tile_body<T, OUT, SPLIT, VEC, true, FOLD>(a, td, lds);
+      tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN>(a, td, lds);
     } else {
-      tile_body<T, OUT, SPLIT, VEC, false, FOLD>(a, td, lds);
+      tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN>(a, td, lds);
     }
     if constexpr (SPLIT > 1) break;
   }
@@ -1036,9 +1048,10 @@ struct fedavg_ctx {
   bool owns_acc = false;
 
   // tiles for SPLIT=1 and SPLIT=4
-  std::vector<TileDesc> tiles1, tiles4;
+  std::vector<TileDesc> tiles1, tiles4, tilesw;  // + kTileWide tiles (whole-layout launches)
   TileDesc* d_tiles1 = nullptr;
   TileDesc* d_tiles4 = nullptr;
+  TileDesc* d_tilesw = nullptr;
   SegDesc* d_segs = nullptr;
   uint32_t* h_flag = nullptr;  // host-coherent pinned NaN words (kernels store into them)
   uint32_t* d_flag = nullptr;  // device alias of h_flag
@@ -1288,45 +1301,53 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
 // own dispatch (its completion signal) instead of a separate marker packet — a marker between
 // two kernels costs ~6-16 µs of queue latency (DESIGN.md §5 traces); the sharded round's
 // per-chunk events use this.
-template <typename T, int OUT, int SPLIT, bool VEC>
+template <typename T, int OUT, int SPLIT, bool VEC, int TILEN = kTile1>
 hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  const int threads = Geo<T, SPLIT>::THREADS;
+  const int threads = Geo<T, SPLIT, TILEN>::THREADS;
   if (fold == FOLD_FMA) {
-    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA>), dim3(nblocks), dim3(threads), 0, s, e0,
-                          e1, 0, a);
+    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA, TILEN>), dim3(nblocks), dim3(threads), 0,
+                          s, e0, e1, 0, a);
   } else if (fold == FOLD_DELTA) {
     if constexpr (SPLIT == 1) {
-      hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA>), dim3(nblocks), dim3(threads), 0, s,
-                            e0, e1, 0, a);
+      hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA, TILEN>), dim3(nblocks),
+                            dim3(threads), 0, s, e0, e1, 0, a);
     } else {
       return hipErrorInvalidValue;  // delta calls run the exact-order kernel only
     }
   } else {
-    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD>), dim3(nblocks), dim3(threads), 0, s,
-                          e0, e1, 0, a);
+    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD, TILEN>), dim3(nblocks), dim3(threads),
+                          0, s, e0, e1, 0, a);
   }
   return hipGetLastError();
 }
 
+// wide = a whole-layout exact-order launch over the kTileWide table (2- / 4-byte inputs only)
 template <typename T, int OUT>
 hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s, hipEvent_t e0,
-                        hipEvent_t e1) {
+                        hipEvent_t e1, bool wide) {
   if (split == 4) {
     return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s, e0, e1)
                : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s, e0, e1);
   }
+  if constexpr (sizeof(T) < 8 && kTileWide > 0) {
+    if (wide) {
+      return vec ? launch_fold<T, OUT, 1, true, kTileWide>(a, fold, nblocks, s, e0, e1)
+                 : launch_fold<T, OUT, 1, false, kTileWide>(a, fold, nblocks, s, e0, e1);
+    }
+  }
+  if (wide) return hipErrorInvalidValue;
   return vec ? launch_fold<T, OUT, 1, true>(a, fold, nblocks, s, e0, e1)
              : launch_fold<T, OUT, 1, false>(a, fold, nblocks, s, e0, e1);
 }
 
 template <int OUT>
 hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s,
-                      hipEvent_t e0, hipEvent_t e1) {
+                      hipEvent_t e0, hipEvent_t e1, bool wide) {
   switch (in_dtype) {
-    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
-    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
-    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
-    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s, e0, e1);
+    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
+    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
+    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
+    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1380,6 +1401,15 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     tb = tb_split1;
     te = te_split1;
   }
+  // whole-layout exact-order launch of a 2- / 4-byte input: the wide table (same elements)
+  const bool wide = split == 1 && c->d_tilesw != nullptr && c->persistent_blocks == 0 && tb_split1 == 0 &&
+                    te_split1 == static_cast<int32_t>(c->tiles1.size()) &&
+                    (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F16 || in_dtype == FEDAVG_BF16);
+  if (wide) {
+    a.tiles = c->d_tilesw;
+    tb = 0;
+    te = static_cast<int>(c->tilesw.size());
+  }
   a.tile_begin = tb;
   a.num_tiles = te - tb;
   if (a.num_tiles <= 0) return FEDAVG_OK;
@@ -1425,9 +1455,9 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   const int fold = st.delta ? FOLD_DELTA
                             : (c->allow_fma && fma_exact_call(st, in_dtype)) ? FOLD_FMA : FOLD_MULADD;
   switch (out_kind) {
-    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1); break;
-    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1); break;
-    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1); break;
+    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide); break;
+    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide); break;
+    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide); break;
     default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
   }
   if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
@@ -1523,6 +1553,7 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   c->valid.assign(num_segments, 0);
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);
+  if (kTileWide > 0) build_tiles(c->seg_numel, kTileWide, c->tilesw);
 #if FEDAVG_PERSISTENT
   {
     int per_cu = 0, cus = 0;
@@ -1563,6 +1594,13 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
     return cleanup(e, "hipMemcpy tiles1");
   if ((e = hipMemcpy(c->d_tiles4, c->tiles4.data(), sizeof(TileDesc) * c->tiles4.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "hipMemcpy tiles4");
+  if (!c->tilesw.empty()) {
+    if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_tilesw), sizeof(TileDesc) * c->tilesw.size())) != hipSuccess)
+      return cleanup(e, "hipMalloc tilesw");
+    if ((e = hipMemcpy(c->d_tilesw, c->tilesw.data(), sizeof(TileDesc) * c->tilesw.size(), hipMemcpyHostToDevice)) !=
+        hipSuccess)
+      return cleanup(e, "hipMemcpy tilesw");
+  }
   if ((e = hipMemcpy(c->d_segs, segs.data(), sizeof(SegDesc) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "hipMemcpy segs");
   std::memset(c->h_flag, 0, sizeof(uint32_t) * 4);
@@ -1596,6 +1634,7 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->d_tiles1) (void)hipFree(c->d_tiles1);
   if (c->d_tiles4) (void)hipFree(c->d_tiles4);
+  if (c->d_tilesw) (void)hipFree(c->d_tilesw);
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->owns_acc && c->acc) (void)hipFree(c->acc);

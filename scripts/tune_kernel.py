@@ -13,7 +13,7 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "t8k": {"FEDAVG_TILE1": 8192},
+    "narrow": {"FEDAVG_TILE_WIDE": 0},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 
@@ -38,6 +38,9 @@ def run_all(rounds=7, iters=10):
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     if len(sys.argv) > 3 and sys.argv[3] == "flat":
         layout = ModelLayout.flat(layout.total_numel)
+    elif len(sys.argv) > 3 and sys.argv[3] != "resnet":
+        from bench import LAYOUTS
+        layout = LAYOUTS[sys.argv[3]]()
     dt = getattr(torch, sys.argv[4]) if len(sys.argv) > 4 else torch.float32
     buckets, views = make_clients(layout, 0, K, dev, dt)
     w = dataset_size_weights(K)

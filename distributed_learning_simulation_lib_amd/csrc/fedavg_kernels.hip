@@ -116,6 +116,12 @@ constexpr int kTile1 = FEDAVG_TILE1;          // 4096 elements, SPLIT = 1 (any d
 #define FEDAVG_TILE_WIDE 8192
 #endif
 constexpr int kTileWide = FEDAVG_TILE_WIDE;
+#ifndef FEDAVG_F64_WIDE  // 1 = fp64 whole-layout launches use the wide table too (A/B knob)
+#define FEDAVG_F64_WIDE 0
+#endif
+#ifndef FEDAVG_AE_F64_WIDE  // elements per lane for fp64 inputs on wide tiles
+#define FEDAVG_AE_F64_WIDE 16
+#endif
 constexpr int kTile4 = (kThreads / 4) * kAE;  // 1024 elements, SPLIT = 4
 
 struct TileDesc {
@@ -349,7 +355,9 @@ struct LaneLoader {
 template <typename T, int SPLIT, int TILEN = kTile1>
 struct Geo {
   static constexpr int AE = (SPLIT > 1) ? kAE
-                          : (sizeof(T) == 2 ? FEDAVG_AE_HALF : sizeof(T) == 8 ? FEDAVG_AE_F64 : kAE);
+                          : (sizeof(T) == 2 ? FEDAVG_AE_HALF
+                             : sizeof(T) == 8 ? (TILEN == kTile1 ? FEDAVG_AE_F64 : FEDAVG_AE_F64_WIDE)
+                                              : kAE);
   static constexpr int LANES = (SPLIT > 1) ? 64 : TILEN / AE;
   static constexpr int THREADS = (SPLIT > 1) ? kThreads : LANES;
   static constexpr int TILE = LANES * AE;
@@ -1329,7 +1337,7 @@ hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nbloc
     return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s, e0, e1)
                : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s, e0, e1);
   }
-  if constexpr (sizeof(T) < 8 && kTileWide > 0) {
+  if constexpr ((sizeof(T) < 8 || FEDAVG_F64_WIDE) && kTileWide > 0) {
     if (wide) {
       return vec ? launch_fold<T, OUT, 1, true, kTileWide>(a, fold, nblocks, s, e0, e1)
                  : launch_fold<T, OUT, 1, false, kTileWide>(a, fold, nblocks, s, e0, e1);
@@ -1404,7 +1412,8 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   // whole-layout exact-order launch of a 2- / 4-byte input: the wide table (same elements)
   const bool wide = split == 1 && c->d_tilesw != nullptr && c->persistent_blocks == 0 && tb_split1 == 0 &&
                     te_split1 == static_cast<int32_t>(c->tiles1.size()) &&
-                    (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F16 || in_dtype == FEDAVG_BF16);
+                    (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F16 || in_dtype == FEDAVG_BF16 ||
+                     (FEDAVG_F64_WIDE && in_dtype == FEDAVG_F64));
   if (wide) {
     a.tiles = c->d_tilesw;
     tb = 0;

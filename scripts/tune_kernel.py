@@ -13,7 +13,8 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "narrow": {"FEDAVG_TILE_WIDE": 0},
+    "d64w16": {"FEDAVG_F64_WIDE": 1, "FEDAVG_AE_F64_WIDE": 16},
+    "d64w16_cu1k": {"FEDAVG_F64_WIDE": 1, "FEDAVG_AE_F64_WIDE": 16, "FEDAVG_CU_BYTES_F64": 1024},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

@@ -18,7 +18,7 @@ from typing import Any
 import torch
 
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout
-from ..message import Message, ModelParameter, ParameterMessage
+from ..message import Message, ModelParameter, is_parameter_message
 from ..quantized import QuantizedTensor, dequantize_tensor
 
 # (device index, layout, split policy) -> context, for the class-level weighted_avg
@@ -148,7 +148,7 @@ class AggregationAlgorithm(ABC):
         device = device or default_device()
         messages = list(data_dict.items())
         first = messages[0][1]
-        assert isinstance(first, ParameterMessage)
+        assert is_parameter_message(first)
         assert first.parameter
         layout = ModelLayout.from_parameters(first.parameter)
         native, keep = split_empty(layout)
@@ -157,7 +157,7 @@ class AggregationAlgorithm(ABC):
         for worker_id, msg in messages:
             r = weights[worker_id] if isinstance(weights, dict) else weights
             assert 0 <= r <= 1
-            assert isinstance(msg, ParameterMessage)
+            assert is_parameter_message(msg)
             assert msg.parameter
             rows.append([msg.parameter[name] for name in layout.names])
             ratios.append(float(r))

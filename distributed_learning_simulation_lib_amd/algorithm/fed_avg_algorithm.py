@@ -33,7 +33,15 @@ import torch
 
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
-from ..message import DeltaParameterMessage, Message, ModelParameter, ParameterMessage
+from ..message import (
+    DeltaParameterMessage,
+    Message,
+    ModelParameter,
+    ParameterMessage,
+    is_delta_message,
+    is_parameter_message,
+    wire_class,
+)
 from ..quantized import QuantizedTensor, dequantize_tensor, record_layout
 from .aggregation_algorithm import (
     AggregationAlgorithm,
@@ -110,7 +118,16 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_data = self._all_worker_data.get(worker_id, None)
         if worker_data is None:
             return True
-        if isinstance(worker_data, DeltaParameterMessage) and self.accumulate and self._delta_fusable(worker_data):
+        # messages are recognised by their dataclass fields, not by class identity: the
+        # reference's own server passes simulation_lib.message objects (message.py)
+        if is_delta_message(worker_data) and not (self.accumulate and self._delta_fusable(worker_data)):
+            # a delta the fold cannot take (consistency-check fields, or the ratio path keeps
+            # whole updates): restore it on the host exactly as the reference server does
+            # (aggregation_server.py:123-125) and keep the full update in its place
+            assert self._old_parameter is not None, "a delta update needs the cached global model"
+            worker_data = worker_data.restore(self._old_parameter)
+            self._all_worker_data[worker_id] = worker_data
+        if is_delta_message(worker_data):
             # restore() fused into the fold: x = old + delta in the kernel (message.py:40-61)
             assert self._old_parameter is not None
             assert len(worker_data.delta_parameter) == len(self._old_parameter)
@@ -123,7 +140,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             worker_data.delta_parameter = {}
             self._stage_client(delta=True)
             return True
-        if not isinstance(worker_data, ParameterMessage):
+        if not is_parameter_message(worker_data):
             return True
         self.__row = {}
         for name, parameter in worker_data.parameter.items():
@@ -403,7 +420,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             other_data |= self.__aggregate_loss(self._all_worker_data)
         other_data |= self.__check_and_reduce_other_data(self._all_worker_data)
         first = next(iter(self._all_worker_data.values()))
-        return ParameterMessage(
+        # the caller's own ParameterMessage class: the reference server matches the result
+        # with `case ParameterMessageBase()` (aggregation_server.py:87) and caches it (:148-167)
+        return wire_class(first, "ParameterMessage")(
             parameter=parameter,
             end_training=first.end_training,
             in_round=first.in_round,

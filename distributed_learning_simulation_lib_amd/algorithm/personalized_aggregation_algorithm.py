@@ -27,7 +27,7 @@ import torch
 from .. import _native
 from ..fedavg import ModelLayout, NaNAggregationError
 from ..ingest import HostIngest
-from ..message import Message, ModelParameter, MultipleWorkerMessage, ParameterMessage
+from ..message import Message, ModelParameter, MultipleWorkerMessage, ParameterMessage, is_parameter_message, wire_class
 from ..personalized import PersonalizedContext
 from .aggregation_algorithm import (
     AggregationAlgorithm,
@@ -74,7 +74,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             return True  # every receiver records a skipped worker (aggregation_algorithm.py:98-100)
         if not any(j != worker_id for j in self._worker_weights):
             return True  # nobody else receives it: the reference never touches it
-        assert isinstance(worker_data, ParameterMessage)
+        assert is_parameter_message(worker_data)
         if self.__layout is None:
             self.__layout = ModelLayout.from_parameters(worker_data.parameter)
         unknown = [k for k in worker_data.parameter if k not in self.__layout.names]
@@ -115,6 +115,10 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         layout = self.__layout
         assert layout is not None
         parameters, central = self._reduce(receivers)
+        # answer in the caller's wire classes (the reference server matches
+        # `case MultipleWorkerMessage()`, aggregation_server.py:84-86)
+        like = self.__arrivals[0][1] if self.__arrivals else None
+        param_cls = wire_class(like, "ParameterMessage")
         results: dict[int, ParameterMessage] = {}
         for j in receivers:
             # the receiver's FedAVGAlgorithm keeps _all_worker_data[worker_id] = update: a worker
@@ -123,13 +127,14 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             for n in folded[j]:
                 by_id[self.__arrivals[n][0]] = self.__arrivals[n][1]
             msgs = list(by_id.values())
-            results[j] = ParameterMessage(
+            results[j] = param_cls(
                 parameter=parameters[j],
                 end_training=msgs[0].end_training,
                 in_round=msgs[0].in_round,
                 other_data=self._check_and_reduce_other_data(msgs),
             )
-        return MultipleWorkerMessage(worker_data=results, other_data={"centralized_parameter": central})
+        return wire_class(like, "MultipleWorkerMessage")(worker_data=results,
+                                                         other_data={"centralized_parameter": central})
 
     def _reduce(self, receivers: list[int]) -> tuple[dict[int, ModelParameter], ModelParameter]:
         layout = self.__layout

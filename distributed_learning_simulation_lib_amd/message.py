@@ -11,6 +11,7 @@ from ``cyy_torch_toolbox``).
 from __future__ import annotations
 
 import copy
+import sys
 from collections.abc import Mapping
 from dataclasses import dataclass, field, fields
 from typing import Any
@@ -90,6 +91,62 @@ class FeatureMessage(Message):
 @dataclass(kw_only=True, slots=True)
 class MultipleWorkerMessage(Message):
     worker_data: Mapping[int, Message]
+
+
+# ---- structural recognition --------------------------------------------------------------
+# The algorithms are handed messages by whichever server hosts them: this package's
+# AggregationServer, or the reference's own (simulation_lib/server/aggregation_server.py:117-130),
+# which passes simulation_lib.message objects. Those are a different class hierarchy with the same
+# dataclass schema, so the plugins recognise a message by its fields, never by class identity,
+# and answer with the ParameterMessage / MultipleWorkerMessage class of the caller's module (the
+# reference server dispatches on `case ParameterMessageBase()` / `case MultipleWorkerMessage()`,
+# aggregation_server.py:83-87, and `isinstance(result, ParameterMessageBase)`, :148).
+_FIELD_CACHE: dict[type, frozenset[str]] = {}
+
+
+def _field_names(obj: Any) -> frozenset[str]:
+    cls = type(obj)
+    names = _FIELD_CACHE.get(cls)
+    if names is None:
+        dc = getattr(cls, "__dataclass_fields__", None)
+        names = frozenset(dc) if dc is not None else frozenset()
+        _FIELD_CACHE[cls] = names
+    return names
+
+
+def is_message(obj: Any) -> bool:
+    """A Message of any wire module (message.py:11-16 fields)."""
+    return {"other_data", "in_round", "end_training", "aggregation_weight"} <= _field_names(obj)
+
+
+def is_parameter_message_base(obj: Any) -> bool:
+    """ParameterMessageBase (message.py:19-21): a Message with ``is_initial``."""
+    return is_message(obj) and "is_initial" in _field_names(obj)
+
+
+def is_parameter_message(obj: Any) -> bool:
+    """ParameterMessage (message.py:24-31): a full update, ``parameter`` dict of tensors."""
+    names = _field_names(obj)
+    return "parameter" in names and "delta_parameter" not in names and is_parameter_message_base(obj)
+
+
+def is_delta_message(obj: Any) -> bool:
+    """DeltaParameterMessage (message.py:34-61): ``delta_parameter`` against the cached model."""
+    return "delta_parameter" in _field_names(obj) and is_parameter_message_base(obj)
+
+
+def wire_class(like: Any, name: str) -> type:
+    """The class ``name`` ("ParameterMessage", "MultipleWorkerMessage", ...) of the wire module
+    ``like`` comes from; this package's class when ``like`` is None or its module has none."""
+    if like is not None:
+        for cls in type(like).__mro__:
+            if cls.__name__ == name and hasattr(cls, "__dataclass_fields__"):
+                return cls
+        mod = sys.modules.get(type(like).__module__)
+        cls = getattr(mod, name, None) if mod is not None else None
+        if isinstance(cls, type) and hasattr(cls, "__dataclass_fields__"):
+            return cls
+    return globals()[name]
 
 
 def _count_tensor_bytes(obj: Any) -> int:

@@ -26,7 +26,14 @@ from typing import Any
 
 import torch
 
-from ..message import DeltaParameterMessage, Message, ParameterMessage, ParameterMessageBase
+from ..message import (
+    Message,
+    ParameterMessage,
+    is_delta_message,
+    is_parameter_message,
+    is_parameter_message_base,
+    wire_class,
+)
 from ..quantized import dequantize_parameter, is_quantized
 
 
@@ -128,18 +135,18 @@ class AggregationServer:
         if data is not None:
             if data.end_training:
                 self._stop = True
-                if not isinstance(data, ParameterMessageBase):
+                if not is_parameter_message_base(data):
                     return
             old_parameter = self._model_cache.parameter
             self._dequantize_if_needed(data)
-            if isinstance(data, DeltaParameterMessage):
+            if is_delta_message(data):
                 assert old_parameter is not None
                 if getattr(self._algorithm, "accepts_delta_messages", False):
                     # the algorithm fuses restore() into its fold (fedavg_*_delta)
                     self._algorithm.set_old_parameter(old_parameter)
                 else:
                     data = data.restore(old_parameter)
-            elif isinstance(data, ParameterMessage):
+            elif is_parameter_message(data):
                 if old_parameter is not None:
                     data.complete(old_parameter)
         self._algorithm.process_worker_data(worker_id=worker_id, worker_data=data)
@@ -155,10 +162,10 @@ class AggregationServer:
         are dequantised before the algorithm sees them — unless the algorithm folds QSGD
         records itself (FedAVGAlgorithm: dequantisation fused into the kernel). Deltas are
         always dequantised (the delta fold takes dense tensors)."""
-        if isinstance(data, DeltaParameterMessage):
+        if is_delta_message(data):
             if is_quantized(data.delta_parameter):
                 data.delta_parameter = dequantize_parameter(data.delta_parameter)
-        elif isinstance(data, ParameterMessage) and is_quantized(data.parameter):
+        elif is_parameter_message(data) and is_quantized(data.parameter):
             if not getattr(self._algorithm, "accepts_quantized_messages", False):
                 data.parameter = dequantize_parameter(data.parameter)
 
@@ -167,10 +174,10 @@ class AggregationServer:
         return self._algorithm.aggregate_worker_data()
 
     def _send_result(self, result: Message) -> None:
-        if isinstance(result, ParameterMessage):
+        if is_parameter_message(result):
             self._model_cache.cache_parameter(result.parameter)
             # what crosses the process boundary is the cached host copy
-            result = ParameterMessage(
+            result = wire_class(result, "ParameterMessage")(
                 parameter=self._model_cache.parameter or {},
                 end_training=result.end_training,
                 in_round=result.in_round,

@@ -17,12 +17,13 @@ import numpy as np
 import pytest
 import torch
 
+import tests.foreign_messages as foreign
 from distributed_learning_simulation_lib_amd import (
-    DeltaParameterMessage,
     FedAVGAlgorithm,
     NaNAggregationError,
     ParameterMessage,
 )
+from distributed_learning_simulation_lib_amd import message as _pkg_message
 from distributed_learning_simulation_lib_amd.algorithm import AggregationAlgorithm
 from distributed_learning_simulation_lib_amd.fedavg import ClientTable, FedAvgContext, ModelLayout, bw_probe
 from oracle.fedavg_oracle import as_f64, fedavg_flat
@@ -33,7 +34,11 @@ CASES = load_golden()
 TORCH_DT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16, "float64": torch.float64}
 
 
-def run_hip(case, device, wave_size, from_host=False, split_policy=1):
+def run_hip(case, device, wave_size, from_host=False, split_policy=1, wire=None, delta_checks=False):
+    """Drive the plugin like AggregationServer does. ``wire``: the message module (default this
+    package's; tests.foreign_messages = another class hierarchy with the same schema, as the
+    reference server passes). ``delta_checks``: deltas carry new_parameter (not fusable)."""
+    wire = wire or _pkg_message
     ptw = case.per_tensor_weight
     if ptw is not None:
         class PerTensor(FedAVGAlgorithm):
@@ -55,10 +60,12 @@ def run_hip(case, device, wave_size, from_host=False, split_policy=1):
             continue
         params = case.torch_params(a, "cpu" if from_host else device)
         if kind == "delta":
-            msg = DeltaParameterMessage(delta_parameter=params, aggregation_weight=a.weight,
-                                        other_data=dict(a.other_data))
+            msg = wire.DeltaParameterMessage(delta_parameter=params, aggregation_weight=a.weight,
+                                             other_data=dict(a.other_data))
+            if delta_checks:
+                msg.new_parameter = {k: old[k] + v.double().cpu() for k, v in params.items()}
         else:
-            msg = ParameterMessage(parameter=params, aggregation_weight=a.weight, other_data=dict(a.other_data))
+            msg = wire.ParameterMessage(parameter=params, aggregation_weight=a.weight, other_data=dict(a.other_data))
             if old is not None:
                 msg.complete(old)
         algo.process_worker_data(a.worker_id, msg)
@@ -85,6 +92,63 @@ def test_plugin_matches_reference_bitwise(name, wave_size, hip_device):
         assert bits_equal(got.cpu().numpy(), want), f"{name}/{k}"
     assert res.other_data == case.meta["result_other_data"]
     assert res.in_round == case.meta["in_round"] and res.end_training == case.meta["end_training"]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_plugin_with_foreign_messages_bitwise(name, hip_device):
+    """Messages of another wire module (the reference server passes simulation_lib.message
+    objects): recognised by their fields, answered in their own ParameterMessage class."""
+    case = CASES[name]
+    if case.error is not None:
+        exc = {"AssertionError": AssertionError, "RuntimeError": RuntimeError}[case.error]
+        with pytest.raises(exc):
+            run_hip(case, hip_device, 3, wire=foreign)
+        return
+    res = run_hip(case, hip_device, 3, from_host=True, wire=foreign)
+    assert type(res) is foreign.ParameterMessage
+    assert list(res.parameter.keys()) == case.meta["out_keys"]
+    for k, want in case.expected.items():
+        assert bits_equal(res.parameter[k].cpu().numpy(), want), f"{name}/{k}"
+    assert res.other_data == case.meta["result_other_data"]
+
+
+@pytest.mark.parametrize("wire", [None, foreign], ids=["pkg", "foreign"])
+def test_unfusable_deltas_are_restored_bitwise(wire, hip_device):
+    """Deltas carrying new_parameter (restore()'s consistency check) take the host restore, then
+    the ordinary fold: still the reference's bits (golden case delta_restore)."""
+    case = CASES["delta_restore"]
+    res = run_hip(case, hip_device, 2, from_host=True, wire=wire, delta_checks=True)
+    for k, want in case.expected.items():
+        assert bits_equal(res.parameter[k].cpu().numpy(), want), k
+
+
+def test_deltas_on_the_ratio_path(hip_device):
+    """accumulate=False with delta updates: restored, then weighted_avg (oracle restatement)."""
+    from oracle import fedavg_oracle as O
+
+    case = CASES["delta_restore"]
+    algo = FedAVGAlgorithm(device=hip_device)
+    algo.accumulate = False
+    old = {k: torch.from_numpy(v.copy()) for k, v in case.old.items()}
+    algo.set_old_parameter(old)
+    odata = {}
+    for a, kind in zip(case.arrivals, case.kinds):
+        params = case.torch_params(a, "cpu")  # workers send host tensors
+        host = {k: v.cpu().numpy() for k, v in params.items()}
+        if kind == "delta":
+            algo.process_worker_data(a.worker_id, _pkg_message.DeltaParameterMessage(
+                delta_parameter=params, aggregation_weight=a.weight))
+            host = O.restore(host, case.old)
+        else:
+            msg = ParameterMessage(parameter=params, aggregation_weight=a.weight)
+            msg.complete(old)
+            algo.process_worker_data(a.worker_id, msg)
+            O.complete(host, case.old)
+        odata[a.worker_id] = O.OracleMessage(parameter=host, aggregation_weight=a.weight)
+    res = algo.aggregate_worker_data()
+    want = O.weighted_avg(odata, O.get_ratios(odata))
+    for k in want:
+        assert bits_equal(res.parameter[k].cpu().numpy(), want[k]), k
 
 
 def test_nan_input_names_the_client(hip_device):

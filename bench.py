@@ -8,9 +8,11 @@ BASELINE.json metric: "aggregated GB/s (device-resident), N-client weighted FedA
        params each), weights = client dataset sizes; one fused HIP launch folds the clients
        in fp64 and writes the fp32 global model; the NaN flag is read back (the reference's
        assertions) — the step ends when the host knows the round is valid.
-  N>1  (BASELINE config 3 at N=4): weak scaling, 64 clients per GPU; every rank folds its
-       shard into an fp64 partial, RCCL reduces the partials to rank 0 in chunks overlapped
-       with the partial kernels, rank 0 finalizes each chunk as it lands.
+  N>1  (BASELINE config 3): strong scaling, 256 clients in total sharded over the N ranks
+       (256/N each); every rank folds its shard into an fp64 partial in tile chunks, RCCL
+       exchanges each chunk while the next one is computed, and rank 0 ends with the fp32
+       global model (DESIGN.md §5). --weak: --clients-per-gpu clients on every rank instead;
+       --total-clients 256 at N=1 is the same-N single-GPU anchor.
 
 value = algorithmic bytes of the whole job (all clients' reads + the output write) / step
 time (max over ranks). Inputs are resident in HBM before the timed region. The
@@ -45,7 +47,12 @@ from distributed_learning_simulation_lib_amd.fedavg import (  # noqa: E402
     OutputTable,
     bw_probe,
 )
-from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, RcclComm, sharded_reduce  # noqa: E402
+from distributed_learning_simulation_lib_amd.sharded import (  # noqa: E402
+    HipLocalReducer,
+    RcclComm,
+    resolve_exchange,
+    sharded_reduce,
+)
 
 METRIC = "aggregated GB/s (device-resident), N-client weighted FedAvg reduce, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -171,40 +178,46 @@ def hbm_probes(device: torch.device, nbytes: int = 4 << 30) -> dict:
     return out
 
 
-def cpu_baseline(layout: ModelLayout, budget_s: float = 12.0, sample_clients: int = 8) -> dict:
-    """Reference CPU op sequence on a bounded sample of the same workload (rank 0, N=1)."""
+def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3) -> dict:
+    """The reference's CPU path on the host cores, rank 0, N=1: the reference's
+    FedAVGAlgorithm call sequence (oracle/ref_torch_cpu.py: process_worker_data per client with
+    its torch CPU ops, then aggregate_worker_data) over ``n_clients`` pre-built messages of the
+    headline workload (64 x ResNet-18 fp32, dataset-size weights), best of ``repeats``."""
     sys.path.insert(0, str(REPO))
-    from oracle.ref_torch_cpu import RefOpsFedAvg
+    from distributed_learning_simulation_lib_amd.message import ParameterMessage
+    from oracle.ref_torch_cpu import RefFedAvgAlgorithm
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    weights = dataset_size_weights(sample_clients)
-    g = torch.Generator().manual_seed(1234)
-    clients = [
-        {n: torch.randn(s, generator=g, dtype=torch.float32) for n, s in zip(layout.names, layout.shapes)}
-        for _ in range(sample_clients)
-    ]
-    nbytes = (sample_clients + 1) * layout.total_numel * 4
+    weights = dataset_size_weights(n_clients)
+    clients = []
+    for i in range(n_clients):  # generation is outside the timed region
+        g = torch.Generator().manual_seed(1234 + i)
+        clients.append({n: torch.randn(s, generator=g, dtype=torch.float32) for n, s in zip(layout.names, layout.shapes)})
+    nbytes = n_clients * layout.total_numel * 4 + layout.total_numel * 4
     times = []
     t_start = time.perf_counter()
-    while time.perf_counter() - t_start < budget_s and len(times) < 1000:
-        algo = RefOpsFedAvg()
+    for _ in range(repeats):
+        msgs = [ParameterMessage(parameter=dict(c), aggregation_weight=w) for c, w in zip(clients, weights)]
+        algo = RefFedAvgAlgorithm()
         t0 = time.perf_counter()
-        for c, w in zip(clients, weights):
-            algo.add(c, w)
-        out = algo.finish()
-        out = {k: v.to(torch.float32) for k, v in out.items()}
+        for wid, m in enumerate(msgs):
+            algo.process_worker_data(wid, m)
+        out = algo.aggregate_worker_data()
         times.append(time.perf_counter() - t0)
+        del out, algo, msgs
     best = min(times)
     return {
         "value": round(nbytes / best / 1e9, 3),
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
+        "seconds_per_round": round(best, 4),
         "sample": (
-            f"{sample_clients} clients x ResNet-18 layout fp32 (62 tensors, 11,689,512 params), "
-            f"reference op sequence (isnan, to(f64)*w, +=, /W, isnan) in torch CPU, "
-            f"best of {len(times)} runs over {time.perf_counter() - t_start:.1f} s"
+            f"the full headline round: {n_clients} pre-built ParameterMessages x {layout.num_segments}-tensor layout "
+            f"({layout.total_numel:,} fp32 params), the reference's FedAVGAlgorithm call sequence "
+            f"(process_worker_data x {n_clients}: isnan, to(f64)*w, +=; aggregate_worker_data: isnan, /W, isnan) "
+            f"in torch CPU ops, best of {repeats} ({time.perf_counter() - t_start:.1f} s)"
         ),
     }
 
@@ -518,7 +531,13 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layout", default="resnet18", choices=sorted(LAYOUTS))
-    ap.add_argument("--clients-per-gpu", type=int, default=64)
+    ap.add_argument("--clients-per-gpu", type=int, default=64,
+                    help="weak scaling (--weak) and the personalized / qsgd workloads: clients per GPU")
+    ap.add_argument("--total-clients", type=int, default=0,
+                    help="clients of the whole job, sharded over the ranks (0 = auto: 64 on one GPU = "
+                         "BASELINE config 2; 256 on N > 1 GPUs = BASELINE config 3, strong scaling)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling instead: --clients-per-gpu clients on every rank")
     ap.add_argument("--wave", type=int, default=0, help="clients per launch (streaming waves); 0 = all")
     ap.add_argument("--chunks", type=int, default=0,
                     help="tile chunks of the sharded reduce (0 = auto: 4 when world > 1 — "
@@ -526,6 +545,9 @@ def main() -> int:
     ap.add_argument("--comm", default="native", choices=["native", "torch"],
                     help="sharded path: the library's own RCCL communicator, whole round in one native "
                          "call (native) or the chunks' reduces through torch.distributed (torch)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "reduce", "scatter"],
+                    help="multi-GPU exchange of the fp64 partials: reduce to rank 0, or reduce-scatter + "
+                         "per-rank finalize + gather (auto: scatter at 2 ranks, reduce above; DESIGN.md §5)")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -569,13 +591,22 @@ def main() -> int:
     layout = LAYOUTS[args.layout]()
     P = layout.total_numel
     T = layout.num_segments
-    n_local = args.clients_per_gpu
-    n_total = n_local * world
+    if args.weak:
+        n_total = args.clients_per_gpu * world
+    elif args.total_clients > 0:
+        n_total = args.total_clients
+    else:
+        n_total = 256 if world > 1 else 64  # BASELINE.json configs[2] / configs[1]
+    # contiguous client shards: rank r folds clients [lo, hi) (N/G each; the dispatcher's split)
+    lo, hi = rank * n_total // world, (rank + 1) * n_total // world
+    n_local = hi - lo
+    if n_local < 1:
+        raise SystemExit(f"{n_total} clients cannot be sharded over {world} ranks")
     wave = args.wave if 0 < args.wave < n_local else n_local
     weights_all = dataset_size_weights(n_total)
-    my_weights = weights_all[rank * n_local : (rank + 1) * n_local]
+    my_weights = weights_all[lo:hi]
 
-    buckets, views = make_clients(layout, rank * n_local, n_local, device, in_dtype)
+    buckets, views = make_clients(layout, lo, n_local, device, in_dtype)
     tables = []
     for w0 in range(0, n_local, wave):
         t = ClientTable(T)
@@ -603,13 +634,15 @@ def main() -> int:
             print(f"warning: native RCCL communicator unavailable ({e}); using --comm torch", file=sys.stderr)
             args.comm = "torch"
 
+    exchange = resolve_exchange(args.exchange, world)
+
     def step() -> None:
         h0 = time.perf_counter()
+        # rank 0 ends the round on the host: sharded_reduce reads the NaN flags there (the
+        # reference's assertions, fed_avg_algorithm.py:35,93,97)
         sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals,
-                       force_collective=args.force_collective, comm=comm)
+                       force_collective=args.force_collective, comm=comm, exchange=exchange)
         host_enqueue[0] += time.perf_counter() - h0
-        if rank == 0:
-            ctx.raise_on_nan()  # the reference's assertions: the round ends on the host
 
     for _ in range(args.warmup):
         step()
@@ -644,6 +677,7 @@ def main() -> int:
     step_s = elapsed / args.steps
     value_gbps = job_bytes / step_s / 1e9
 
+    n_local_max = max(((r + 1) * n_total // world) - (r * n_total // world) for r in range(world))
     # dominant kernel family, per step on this rank: the client reads + the result write
     # (fused single launch) or + the fp64 partial/accumulator traffic (waves, shards)
     n_waves = len(tables)
@@ -707,6 +741,20 @@ def main() -> int:
     if rank != 0:
         return 0
     short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    workload = f"fedavg_{args.layout}_{short}_{n_total}_clients"
+    if world > 1:
+        workload += f"_sharded_over_{world}_gpus" + ("_weak" if args.weak else "")
+    if n_waves > 1:
+        workload += f"_waves_of_{wave}"
+    if args.layout == "resnet18" and not args.weak and n_total == 64 and world == 1:
+        baseline_config = "BASELINE.json configs[1]"
+    elif args.layout == "resnet18" and not args.weak and n_total == 256:
+        baseline_config = ("BASELINE.json configs[2] (256 clients sharded over the GPUs, strong scaling)" if world > 1
+                           else "BASELINE.json configs[2] on one GPU (the same-N anchor of the 2/4/8-GPU lines)")
+    elif args.layout == "resnet18" and args.weak:
+        baseline_config = f"BASELINE.json configs[2] weak-scaled ({n_local} clients per GPU)"
+    else:
+        baseline_config = "see DESIGN.md"
     line = {
         "metric": METRIC,
         "value": round(value_gbps, 2),
@@ -716,13 +764,13 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
         "config": {
-            "workload": f"fedavg_{args.layout}_{short}_{n_local}_clients_per_gpu" + (f"_waves_of_{wave}" if n_waves > 1 else ""),
-            "clients_per_gpu": n_local,
+            "workload": workload,
+            "clients_per_gpu": n_local_max,
             "total_clients": n_total,
             "clients_per_launch": wave,
             "client_table": "re-staged every round" if args.no_plan else "prepared once (persistent client slots)",
@@ -731,16 +779,16 @@ def main() -> int:
             "in_dtype": args.in_dtype,
             "accumulate_dtype": "float64",
             "out_dtype": args.out_dtype,
-            "parallelism": "single GPU" if world == 1 else f"clients sharded over {world} GPUs + chunked RCCL reduce to rank 0",
+            "parallelism": "single GPU" if world == 1 else (
+                f"clients sharded over {world} GPUs + chunked RCCL "
+                + ("reduce to rank 0" if exchange == "reduce" else "reduce-scatter, per-rank finalize, gather to rank 0")),
             "exchange": None if not sharded else {
-                "chunks": args.chunks, "comm": args.comm,
+                "mode": exchange, "chunks": args.chunks, "comm": args.comm,
                 "partial_only_ms_per_step": None if partial_only_ms is None else round(partial_only_ms, 4),
                 "exposed_exchange_and_finalize_ms": (None if partial_only_ms is None
                                                      else round(step_s * 1e3 - partial_only_ms, 4)),
             },
-            "baseline_config": ("BASELINE.json configs[1]" if (world == 1 and args.layout == "resnet18" and n_local == 64)
-                                else "BASELINE.json configs[2] (weak-scaled, 64 clients/GPU)" if args.layout == "resnet18"
-                                else "see DESIGN.md"),
+            "baseline_config": baseline_config,
         },
         "roofline": {
             "bound": "hbm",

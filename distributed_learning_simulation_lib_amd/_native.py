@@ -31,6 +31,9 @@ FLAG_ACC_NAN = 0x1
 FLAG_RESULT_NAN = 0x2
 FLAG_CENTRAL_NAN = 0x4
 ABI_VERSION = 1
+ACC_ALIGN = 32  # FEDAVG_ACC_ALIGN: accumulator segments start at multiples of 32 elements
+BUILD_ABLATE_EPILOGUE = 0x1
+BUILD_ABLATE_QSGD = 0x2
 
 _PP = POINTER(c_void_p)
 _PD = POINTER(c_double)
@@ -38,6 +41,8 @@ _PD = POINTER(c_double)
 # name -> (restype, argtypes); the full exported surface of the library
 SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_abi_version": (c_int32, []),
+    "fedavg_build_flags": (c_int32, []),
+    "fedavg_layout_acc_numel": (c_int64, [POINTER(c_int64), c_int32]),
     "fedavg_last_error": (ctypes.c_char_p, []),
     "fedavg_qsgd_record_bytes": (c_int64, [c_int64]),
     "fedavg_qsgd_sign_offset": (c_int64, [c_int64]),
@@ -93,6 +98,9 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_plan_create_finalize": (c_int32, [c_void_p, _PD, _PP, c_int32, POINTER(c_void_p)]),
     "fedavg_plan_run_range": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_plan_destroy": (c_int32, [c_void_p]),
+    "fedavg_plan_finalize_window": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "fedavg_plan_copy_out": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "fedavg_plan_out_dtype": (c_int32, [c_void_p]),
     "fedavg_check": (c_int32, [c_void_p, c_void_p, POINTER(c_uint32)]),
     "fedavg_find_nan_clients": (
         c_int32,
@@ -121,6 +129,8 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_comm_create": (c_int32, [_PP, c_void_p, c_int32, c_int32, c_int32]),
     "fedavg_comm_destroy": (c_int32, [c_void_p]),
     "fedavg_sharded_round": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "fedavg_sharded_round_scatter": (
+        c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
 }
 
 _lib: ctypes.CDLL | None = None
@@ -134,8 +144,11 @@ class NativeError(RuntimeError):
         self.status = status
 
 
-def load(path: str | None = None) -> ctypes.CDLL:
-    """Load the in-tree HIP library (raises if it is absent — there is no fallback)."""
+def load(path: str | None = None, allow_ablated: bool = False) -> ctypes.CDLL:
+    """Load the in-tree HIP library (raises if it is absent — there is no fallback).
+
+    A timing-only ablation build (``fedavg_build_flags() != 0``: results wrong by design) is
+    refused unless ``allow_ablated`` or ``FEDAVG_ALLOW_ABLATED=1`` (the A/B scripts)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -154,6 +167,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
         fn.argtypes = argtypes
     if lib.fedavg_abi_version() != ABI_VERSION:
         raise ImportError("fedavg_hip ABI version mismatch")
+    flags = lib.fedavg_build_flags()
+    if flags and not (allow_ablated or os.environ.get("FEDAVG_ALLOW_ABLATED") == "1"):
+        raise ImportError(
+            f"{lib_path} is a timing-only ablation build (fedavg_build_flags = {flags:#x}: "
+            "its results are wrong by design); set FEDAVG_ALLOW_ABLATED=1 to load it for A/B timing"
+        )
     if path is None:
         _lib = lib
     return lib

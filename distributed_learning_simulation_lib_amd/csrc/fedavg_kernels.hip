@@ -1041,6 +1041,79 @@ __global__ __launch_bounds__(kThreads) void bw_read_kernel(const f32x4* __restri
   if (x == 0x9e3779b9u) dst[blockIdx.x] = x;  // practically never taken; keeps loads live
 }
 
+// ---------------------------------------------------------------------------------------
+// Scatter exchange of the multi-GPU round (sharded_comm.cpp): after the fp64
+// partials are reduce-scattered, rank r holds the global sums of an element window [lo, hi) of
+// the accumulator (any alignment, may span segments and their padding). It divides its window by
+// the per-segment total weights (_apply_total_weight, fed_avg_algorithm.py:71-74, with the :93 /
+// :97 NaN checks) into a result buffer kept in accumulator coordinates; the windows are gathered
+// to the root, which copies the result into the caller's per-segment outputs.
+// ---------------------------------------------------------------------------------------
+constexpr int kWinElems = 8;  // contiguous elements per lane of the window kernel
+
+template <typename O>
+__global__ __launch_bounds__(kThreads) void window_finalize_kernel(const double* __restrict__ src, int64_t lo,
+                                                                   int64_t n, const SegDesc* __restrict__ segs,
+                                                                   int32_t T, const double* __restrict__ wtot,
+                                                                   O* __restrict__ res, uint32_t* flag) {
+  const int64_t e0 = (static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x) * kWinElems;
+  bool bad_acc = false, bad_res = false;
+  if (e0 < n) {
+    // segment of the first element: the last segment starting at or before it (binary search)
+    const int64_t p0 = lo + e0;
+    int s = 0, hi_s = T - 1;
+    while (s < hi_s) {
+      const int mid = (s + hi_s + 1) >> 1;
+      if (segs[mid].acc_off <= p0) s = mid;
+      else hi_s = mid - 1;
+    }
+    int64_t seg_off = segs[s].acc_off, seg_n = segs[s].numel;
+    double W = wtot[s];
+#pragma unroll
+    for (int j = 0; j < kWinElems; ++j) {
+      const int64_t e = e0 + j;
+      if (e >= n) break;
+      const int64_t p = lo + e;
+      while (s + 1 < T && segs[s + 1].acc_off <= p) {
+        ++s;
+        seg_off = segs[s].acc_off;
+        seg_n = segs[s].numel;
+        W = wtot[s];
+      }
+      if (p - seg_off >= seg_n) continue;  // alignment padding between segments
+      const double v = src[e];
+      const double r = v / W;
+      bad_acc |= (v != v);
+      bad_res |= (r != r);
+      res[p] = static_cast<O>(r);
+    }
+  }
+  const uint64_t ba = __ballot(bad_acc), br = __ballot(bad_res);
+  if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+    if (ba) raise_flag(flag, 0);
+    if (br) raise_flag(flag, 1);
+  }
+}
+
+// Root: result (accumulator coordinates) -> the caller's per-segment outputs, one workgroup per
+// tile. A NaN in the gathered result (another rank's :93 / :97 failure) raises the result flag.
+template <typename O>
+__global__ __launch_bounds__(kThreads) void copy_out_kernel(const TileDesc* __restrict__ tiles,
+                                                            const SegDesc* __restrict__ segs,
+                                                            const O* __restrict__ res, void* const* outs,
+                                                            uint32_t* flag) {
+  const TileDesc td = load_tile(tiles, blockIdx.x);
+  const gptr<const O> src = to_global<O>(res + segs[td.seg].acc_off + td.start);
+  const gptr<O> dst = to_global_mut<O>(reinterpret_cast<void*>(to_const<uint64_t>(outs)[td.seg])) + td.start;
+  bool bad = false;
+  for (int i = threadIdx.x; i < td.count; i += kThreads) {
+    const O v = src[i];
+    bad |= (v != v);
+    dst[i] = v;
+  }
+  if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) raise_flag(flag, 1);
+}
+
 }  // namespace
 
 // =======================================================================================
@@ -1523,6 +1596,10 @@ extern "C" {
 
 int32_t fedavg_abi_version(void) { return FEDAVG_ABI_VERSION; }
 
+int32_t fedavg_build_flags(void) {
+  return (FEDAVG_ABLATE_EPILOGUE ? FEDAVG_BUILD_ABLATE_EPILOGUE : 0) | (FEDAVG_QSGD_ABLATE ? FEDAVG_BUILD_ABLATE_QSGD : 0);
+}
+
 int64_t fedavg_qsgd_sign_offset(int64_t numel) {
   if (numel < 0) return -1;
   return 16 + static_cast<int64_t>(align_up(static_cast<size_t>(numel), 16));
@@ -1555,7 +1632,7 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   int64_t off = 0;
   for (int t = 0; t < num_segments; ++t) {
     c->seg_acc_off[t] = off;
-    off += static_cast<int64_t>(align_up(static_cast<size_t>(seg_numel[t]), 2));
+    off += static_cast<int64_t>(align_up(static_cast<size_t>(seg_numel[t]), FEDAVG_ACC_ALIGN));
   }
   c->acc_numel = off;
   c->wsum.assign(num_segments, -0.0);  // additive identity: the first weight is taken as is
@@ -2099,6 +2176,66 @@ int32_t fedavg_plan_create_finalize(fedavg_ctx* c, const double* total_weights, 
   }
   *out = p;
   return FEDAVG_OK;
+}
+
+int64_t fedavg_layout_acc_numel(const int64_t* seg_numel, int32_t num_segments) {
+  if (!seg_numel || num_segments <= 0) return -1;
+  int64_t off = 0;
+  for (int t = 0; t < num_segments; ++t) {
+    if (seg_numel[t] <= 0) return -1;
+    off += static_cast<int64_t>(align_up(static_cast<size_t>(seg_numel[t]), FEDAVG_ACC_ALIGN));
+  }
+  return off;
+}
+
+int32_t fedavg_plan_finalize_window(fedavg_plan* p, const double* src, int64_t lo, int64_t hi, void* res,
+                                    void* stream) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind != fedavg_plan::FINALIZE) return fail(FEDAVG_ERR_INVALID, "a finalize plan is required");
+  fedavg_ctx* c = p->ctx;
+  if (lo < 0 || hi < lo || hi > c->acc_numel) return fail(FEDAVG_ERR_INVALID, "bad accumulator window");
+  if (hi == lo) return FEDAVG_OK;
+  if (!src || !res) return fail(FEDAVG_ERR_INVALID, "null window buffer");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = hi - lo;
+  const int64_t per_block = static_cast<int64_t>(kThreads) * kWinElems;
+  const dim3 grid(static_cast<unsigned>((n + per_block - 1) / per_block)), block(kThreads);
+  if (p->out_kind == OUT_F32) {
+    hipLaunchKernelGGL(window_finalize_kernel<float>, grid, block, 0, s, src, lo, n, c->d_segs, c->T,
+                       p->st.tab.wtot, static_cast<float*>(res), c->d_flag);
+  } else {
+    hipLaunchKernelGGL(window_finalize_kernel<double>, grid, block, 0, s, src, lo, n, c->d_segs, c->T,
+                       p->st.tab.wtot, static_cast<double*>(res), c->d_flag);
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_plan_copy_out(fedavg_plan* p, const void* res, void* stream) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind != fedavg_plan::FINALIZE) return fail(FEDAVG_ERR_INVALID, "a finalize plan is required");
+  if (!res) return fail(FEDAVG_ERR_INVALID, "null result buffer");
+  fedavg_ctx* c = p->ctx;
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(c->tiles1.size())), block(kThreads);
+  if (p->out_kind == OUT_F32) {
+    hipLaunchKernelGGL(copy_out_kernel<float>, grid, block, 0, s, c->d_tiles1, c->d_segs,
+                       static_cast<const float*>(res), p->st.tab.outs, c->d_flag);
+  } else {
+    hipLaunchKernelGGL(copy_out_kernel<double>, grid, block, 0, s, c->d_tiles1, c->d_segs,
+                       static_cast<const double*>(res), p->st.tab.outs, c->d_flag);
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_plan_out_dtype(const fedavg_plan* p) {
+  if (!p) return -1;
+  if (p->out_kind == OUT_F32) return FEDAVG_F32;
+  if (p->out_kind == OUT_F64) return FEDAVG_F64;
+  return -1;
 }
 
 // Shared with sharded_comm.cpp: set the profiling flag, return the previous one (the sharded

@@ -43,6 +43,12 @@ struct Rccl {
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclReduce) reduce = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGather) gather = nullptr;  // RCCL extension; grouped send / recv when absent
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   std::string error;
 };
@@ -77,7 +83,14 @@ Rccl& rccl() {
     r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.handle, "ncclCommDestroy"));
     r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(r.handle, "ncclReduce"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.handle, "ncclGetErrorString"));
-    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.reduce || !r.error_string)
+    r.reduce_scatter = reinterpret_cast<decltype(r.reduce_scatter)>(dlsym(r.handle, "ncclReduceScatter"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(r.handle, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(r.handle, "ncclGroupEnd"));
+    r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(r.handle, "ncclGather"));
+    r.send = reinterpret_cast<decltype(r.send)>(dlsym(r.handle, "ncclSend"));
+    r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(r.handle, "ncclRecv"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.reduce || !r.error_string ||
+        !r.reduce_scatter || !r.group_start || !r.group_end || !r.send || !r.recv)
       r.error = "RCCL library lacks a required symbol";
   });
   return r;
@@ -111,7 +124,64 @@ struct fedavg_comm {
   hipStream_t stream = nullptr;  // high-priority comm stream
   std::vector<hipEvent_t> chunk_events;
   hipEvent_t done = nullptr;
+  // scatter exchange scratch: reduce-scattered fp64 windows (+ the root's chunk tails) and the
+  // finalized result in accumulator coordinates (output dtype)
+  double* slice = nullptr;
+  size_t slice_cap = 0;  // elements
+  char* res = nullptr;
+  size_t res_cap = 0;  // bytes
 };
+
+namespace {
+
+int32_t ensure_events(fedavg_comm* c, int32_t chunks) {
+  while (static_cast<int32_t>(c->chunk_events.size()) < chunks) {
+    hipEvent_t ev = nullptr;
+    COMM_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->chunk_events.push_back(ev);
+  }
+  return FEDAVG_OK;
+}
+
+int32_t ensure_scratch(fedavg_comm* c, hipStream_t s, size_t slice_elems, size_t res_bytes) {
+  if (c->slice_cap >= slice_elems && c->res_cap >= res_bytes) return FEDAVG_OK;
+  COMM_HIP_TRY(hipStreamSynchronize(c->stream));  // an earlier round may still read the old buffers
+  COMM_HIP_TRY(hipStreamSynchronize(s));
+  if (c->slice_cap < slice_elems) {
+    if (c->slice) COMM_HIP_TRY(hipFree(c->slice));
+    c->slice = nullptr;
+    c->slice_cap = 0;
+    COMM_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->slice), std::max<size_t>(slice_elems, 1) * sizeof(double)));
+    c->slice_cap = slice_elems;
+  }
+  if (c->res_cap < res_bytes) {
+    if (c->res) COMM_HIP_TRY(hipFree(c->res));
+    c->res = nullptr;
+    c->res_cap = 0;
+    COMM_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->res), std::max<size_t>(res_bytes, 16)));
+    c->res_cap = res_bytes;
+  }
+  return FEDAVG_OK;
+}
+
+// Root gathers every rank's count-element window: rank i's lands at recv + i * count elements.
+ncclResult_t gather_windows(fedavg_comm* c, const char* send, char* recv, size_t count, size_t elem,
+                            ncclDataType_t dt, int32_t root) {
+  Rccl& r = rccl();
+  if (r.gather) return r.gather(send, recv, count, dt, root, c->nccl, c->stream);
+  ncclResult_t res = r.group_start();
+  if (res != ncclSuccess) return res;
+  if (c->rank == root) {
+    for (int32_t i = 0; i < c->world && res == ncclSuccess; ++i)
+      if (i != root) res = r.recv(recv + static_cast<size_t>(i) * count * elem, count, dt, i, c->nccl, c->stream);
+  } else {
+    res = r.send(send, count, dt, root, c->nccl, c->stream);
+  }
+  const ncclResult_t end = r.group_end();
+  return res != ncclSuccess ? res : end;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -163,6 +233,8 @@ int32_t fedavg_comm_destroy(fedavg_comm* c) {
   if (c->nccl) (void)rccl().comm_destroy(c->nccl);
   for (hipEvent_t ev : c->chunk_events) (void)hipEventDestroy(ev);
   if (c->done) (void)hipEventDestroy(c->done);
+  if (c->slice) (void)hipFree(c->slice);
+  if (c->res) (void)hipFree(c->res);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return FEDAVG_OK;
@@ -178,11 +250,7 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
   chunks = std::max(1, std::min(chunks, n));
   COMM_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  while (static_cast<int32_t>(c->chunk_events.size()) < chunks) {
-    hipEvent_t ev = nullptr;
-    COMM_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    c->chunk_events.push_back(ev);
-  }
+  if (int32_t st = ensure_events(c, chunks)) return st;
   double* acc = static_cast<double*>(fedavg_accumulator(ctx));
   // with profiling on (fedavg_prof_enable), only the first chunk's launch is timed
   const int32_t prof = fedavg_internal_set_prof(ctx, 0);
@@ -215,6 +283,92 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
   COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
   fedavg_internal_set_prof(ctx, 0);
   if (c->rank == root) return fedavg_plan_run_range(finalize, 0, n, s);
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_sharded_round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                                     int32_t chunks, int32_t root, void* stream) {
+  if (!c || !ctx || !partial || !finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
+  if (root < 0 || root >= c->world) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "bad root");
+  const int32_t odt = fedavg_plan_out_dtype(finalize);
+  if (odt != FEDAVG_F32 && odt != FEDAVG_F64)
+    return fedavg_internal_fail(FEDAVG_ERR_INVALID, "every rank needs a finalize plan (fp32 / fp64 outputs)");
+  const int32_t n = fedavg_num_tiles(ctx);
+  if (n <= 0) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "context has no tiles");
+  chunks = std::max(1, std::min(chunks, n));
+  const int64_t G = c->world;
+  const size_t ob = (odt == FEDAVG_F32) ? 4 : 8;
+  const ncclDataType_t ndt = (odt == FEDAVG_F32) ? ncclFloat32 : ncclFloat64;
+  COMM_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (int32_t st = ensure_events(c, chunks)) return st;
+
+  // geometry: chunk k = tiles [tb, te) = accumulator [A, B); B - A = G*L + R (R = 0 whenever G
+  // divides 32: segments start at multiples of FEDAVG_ACC_ALIGN, tiles at multiples of 4096)
+  struct Piece {
+    int32_t tb, te;
+    int64_t A, L, R, off, rem;
+  };
+  std::vector<Piece> pieces;
+  int64_t slice_elems = 0, rem_elems = 0;
+  for (int32_t k = 0, tb = 0; k < chunks; ++k) {
+    const int32_t te = static_cast<int32_t>((static_cast<int64_t>(n) * (k + 1)) / chunks);
+    if (te <= tb) continue;
+    int64_t a = 0, b = 0;
+    if (int32_t st = fedavg_tile_range(ctx, tb, te, &a, &b)) return st;
+    Piece p{tb, te, a, (b - a) / G, (b - a) % G, slice_elems, rem_elems};
+    slice_elems += p.L;
+    rem_elems += p.R;
+    pieces.push_back(p);
+    tb = te;
+  }
+  const int64_t acc_numel = fedavg_acc_numel(ctx);
+  if (int32_t st = ensure_scratch(c, s, static_cast<size_t>(slice_elems + rem_elems), ob * static_cast<size_t>(acc_numel)))
+    return st;
+  double* acc = static_cast<double*>(fedavg_accumulator(ctx));
+  double* rem_base = c->slice + slice_elems;
+  const int32_t prof = fedavg_internal_set_prof(ctx, 0);
+  struct Restore {
+    fedavg_ctx* ctx;
+    int32_t prof;
+    ~Restore() { fedavg_internal_set_prof(ctx, prof); }
+  } restore{ctx, prof};
+  Rccl& r = rccl();
+  for (size_t k = 0; k < pieces.size(); ++k) {
+    const Piece& p = pieces[k];
+    fedavg_internal_set_prof(ctx, (k == 0) ? prof : 0);
+    hipEvent_t ev = c->chunk_events[k];
+    if (int32_t st = fedavg_internal_plan_run_range(partial, p.tb, p.te, s, &ev)) return st;
+    COMM_HIP_TRY(hipStreamWaitEvent(c->stream, ev, 0));
+    ncclResult_t res = r.group_start();
+    if (res == ncclSuccess && p.L > 0)
+      res = r.reduce_scatter(acc + p.A, c->slice + p.off, static_cast<size_t>(p.L), ncclFloat64, ncclSum, c->nccl,
+                             c->stream);
+    if (res == ncclSuccess && p.R > 0)
+      res = r.reduce(acc + p.A + G * p.L, rem_base + p.rem, static_cast<size_t>(p.R), ncclFloat64, ncclSum, root,
+                     c->nccl, c->stream);
+    const ncclResult_t end = r.group_end();
+    if (res != ncclSuccess) return rccl_fail(res, "ncclReduceScatter");
+    if (end != ncclSuccess) return rccl_fail(end, "ncclGroupEnd");
+    // this rank's window (and the root's share of the tail), divided into the result buffer
+    const int64_t lo = p.A + c->rank * p.L;
+    if (p.L > 0)
+      if (int32_t st = fedavg_plan_finalize_window(finalize, c->slice + p.off, lo, lo + p.L, c->res, c->stream))
+        return st;
+    if (p.R > 0 && c->rank == root)
+      if (int32_t st = fedavg_plan_finalize_window(finalize, rem_base + p.rem, p.A + G * p.L, p.A + G * p.L + p.R,
+                                                   c->res, c->stream))
+        return st;
+    if (p.L > 0) {
+      res = gather_windows(c, c->res + static_cast<size_t>(lo) * ob, c->res + static_cast<size_t>(p.A) * ob,
+                           static_cast<size_t>(p.L), ob, ndt, root);
+      if (res != ncclSuccess) return rccl_fail(res, "ncclGather");
+    }
+  }
+  COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
+  COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
+  fedavg_internal_set_prof(ctx, 0);
+  if (c->rank == root) return fedavg_plan_copy_out(finalize, c->res, s);
   return FEDAVG_OK;
 }
 

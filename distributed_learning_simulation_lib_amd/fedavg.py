@@ -205,7 +205,7 @@ class FedAvgContext:
             raise ValueError("a native layout needs at least one tensor and no empty tensors")
         numels = (ctypes.c_int64 * layout.num_segments)(*layout.numels)
         # the accumulator is a torch tensor so collectives (RCCL) can run on it
-        acc_numel = self._padded_acc_numel(layout)
+        acc_numel = self._padded_acc_numel(layout, self._lib)
         self.accumulator = torch.zeros(acc_numel, dtype=torch.float64, device=device)
         handle = ctypes.c_void_p()
         _native.check(
@@ -223,8 +223,17 @@ class FedAvgContext:
             _native.check(self._lib.fedavg_set_split_policy(self._h, split_policy))
 
     @staticmethod
-    def _padded_acc_numel(layout: ModelLayout) -> int:
-        return layout.padded_offsets(8)[1]
+    def _padded_acc_numel(layout: ModelLayout, lib: ctypes.CDLL) -> int:
+        """Accumulator elements: every segment starts at a multiple of FEDAVG_ACC_ALIGN (32)."""
+        numels = (ctypes.c_int64 * layout.num_segments)(*layout.numels)
+        n = int(lib.fedavg_layout_acc_numel(numels, layout.num_segments))
+        if n < 0:
+            raise ValueError("bad layout")
+        return n
+
+    @property
+    def acc_numel(self) -> int:
+        return self.accumulator.numel()
 
     # -- lifecycle -------------------------------------------------------------------
     def close(self) -> None:
@@ -502,6 +511,27 @@ class AggregatePlan:
 
     def run_range(self, tile_begin: int, tile_end: int) -> None:
         _native.check(self.ctx._lib.fedavg_plan_run_range(self._h, tile_begin, tile_end, self.ctx.stream))
+
+    # -- scatter exchange pieces (finalize plans; sharded.py) ---------------------------
+    @property
+    def out_dtype(self) -> torch.dtype:
+        code = int(self.ctx._lib.fedavg_plan_out_dtype(self._h))
+        return {_native.F32: torch.float32, _native.F64: torch.float64}[code]
+
+    def finalize_window(self, src: torch.Tensor, lo: int, hi: int, res: torch.Tensor) -> None:
+        """res[p] = src[p - lo] / W[seg(p)] over accumulator positions [lo, hi) (padding skipped);
+        ``res`` is in accumulator coordinates, of the plan's out dtype."""
+        if src.dtype != torch.float64 or src.numel() < hi - lo or res.dtype != self.out_dtype \
+                or res.numel() < self.ctx.acc_numel or not (src.is_contiguous() and res.is_contiguous()):
+            raise ValueError("window buffers do not match the plan")
+        _native.check(self.ctx._lib.fedavg_plan_finalize_window(
+            self._h, ctypes.c_void_p(src.data_ptr()), lo, hi, ctypes.c_void_p(res.data_ptr()), self.ctx.stream))
+
+    def copy_out(self, res: torch.Tensor) -> None:
+        """The plan's outputs <- res (accumulator coordinates)."""
+        if res.dtype != self.out_dtype or res.numel() < self.ctx.acc_numel or not res.is_contiguous():
+            raise ValueError("result buffer does not match the plan")
+        _native.check(self.ctx._lib.fedavg_plan_copy_out(self._h, ctypes.c_void_p(res.data_ptr()), self.ctx.stream))
 
     def close(self) -> None:
         if self._h is not None and self._h.value:

@@ -9,10 +9,19 @@ clients are partitioned over the ranks (one process per GPU, ``torch.distributed
     root:    S   = sum_r S_r                            (RCCL reduce, chunked)
     root:    out = S / W                                (HIP finalize kernel, per chunk)
 
-The partial is produced and reduced in chunks of tiles: the kernel for chunk c+1 runs on
-the compute stream while RCCL reduces chunk c on its own stream; the root finalizes every
-tile in one launch once the last reduce has landed. This is the only exchange step of the
-path.
+The partial is produced and exchanged in chunks of tiles: the kernel for chunk c+1 runs on
+the compute stream while RCCL exchanges chunk c on its own stream. Two exchanges (DESIGN.md §5
+cost table), both the one exchange step of the path:
+
+  * ``reduce``:  ncclReduce of each chunk to the root; the root finalizes every tile at the end.
+  * ``scatter``: ncclReduceScatter of each chunk (rank r owns the sums of the chunk's r-th
+    window), every rank divides its own window, ncclGather brings the windows (output dtype)
+    to the root, which copies them into its outputs. Root ingress (G-1)/G x (fp64 partial +
+    result) instead of the whole fp64 partial; all ranks do equal exchange work.
+
+``exchange="auto"`` picks scatter at 2 ranks and reduce above (the cost model of DESIGN.md §5).
+A process group on the ``gloo`` backend with GPU accumulators stages each chunk through host
+memory (tests and hosts without RCCL); ``nccl`` (= RCCL) works on HBM directly.
 
 Numerics: each rank accumulates its clients in arrival order exactly like the single-GPU
 kernel; the cross-rank sum reorders fp64 additions, so results match the reference to fp64
@@ -37,6 +46,17 @@ from . import _native
 from .fedavg import ClientTable, FedAvgContext, OutputTable
 
 
+EXCHANGES = ("auto", "reduce", "scatter")
+
+
+def resolve_exchange(exchange: str, world: int) -> str:
+    if exchange not in EXCHANGES:
+        raise ValueError(f"exchange must be one of {EXCHANGES}, not {exchange!r}")
+    if exchange == "auto":
+        return "scatter" if world == 2 else "reduce"
+    return exchange
+
+
 class LocalReducer(Protocol):
     accumulator: torch.Tensor
 
@@ -54,6 +74,16 @@ class LocalReducer(Protocol):
     def fused(self) -> None: ...
 
     def prefold(self) -> None: ...
+
+    # scatter exchange: window finalize into a result buffer in accumulator coordinates, then
+    # the root's copy into its outputs
+    def result_buffer(self) -> torch.Tensor: ...
+
+    def finalize_window(self, src: torch.Tensor, lo: int, hi: int, res: torch.Tensor) -> None: ...
+
+    def copy_out(self, res: torch.Tensor) -> None: ...
+
+    def raise_on_nan(self) -> None: ...
 
 
 class HipLocalReducer:
@@ -85,6 +115,7 @@ class HipLocalReducer:
         self._partial_plan = None
         self._finalize_plan = None
         self._finalize_totals: list[float] | None = None
+        self._res: torch.Tensor | None = None
 
     @property
     def num_tiles(self) -> int:
@@ -113,12 +144,22 @@ class HipLocalReducer:
     def set_accumulated(self, total_weights: Sequence[float]) -> None:
         totals = [float(w) for w in total_weights]
         if self.use_plan:
-            if self._finalize_plan is None or self._finalize_totals != totals:
-                assert self.outs is not None
-                self._finalize_plan = self.ctx.plan_finalize(totals, self.outs, self.out_dtype)
-                self._finalize_totals = totals
+            self._plan_finalize(totals)
         else:
             self.ctx.set_accumulated(totals)
+
+    def _plan_finalize(self, totals: list[float]) -> None:
+        if self._finalize_plan is None or self._finalize_totals != totals:
+            if self.outs is None:
+                # a non-root rank of the scatter exchange finalizes windows only: its plan needs
+                # outputs of the layout, which it never copies into
+                offs, total = self.ctx.layout.padded_offsets(torch.empty((), dtype=self.out_dtype).element_size())
+                flat = torch.empty(total, dtype=self.out_dtype, device=self.ctx.device)
+                self.outs = OutputTable([flat[o : o + m] for o, m in zip(offs, self.ctx.layout.numels)],
+                                        self.ctx.layout, self.ctx.device, self.out_dtype)
+                self._scratch_outs = True
+            self._finalize_plan = self.ctx.plan_finalize(totals, self.outs, self.out_dtype)
+            self._finalize_totals = totals
 
     def finalize_range(self, tile_begin: int, tile_end: int) -> None:
         assert self.outs is not None
@@ -128,18 +169,44 @@ class HipLocalReducer:
         else:
             self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
 
-    def native_round(self, comm: RcclComm, total_weights: Sequence[float], chunks: int, root: int) -> None:
-        """One round through the library's own RCCL pipeline (``fedavg_sharded_round``): the
-        chunk launches, the reduces and the finalize are enqueued by one native call."""
+    def native_round(self, comm: RcclComm, total_weights: Sequence[float], chunks: int, root: int,
+                     exchange: str = "reduce") -> None:
+        """One round through the library's own RCCL pipeline (``fedavg_sharded_round`` or
+        ``fedavg_sharded_round_scatter``): the chunk launches, the exchange and the finalize are
+        enqueued by one native call."""
         assert self.use_plan and self.table is not None
         if self._partial_plan is None:
             self._partial_plan = self.ctx.plan_partial(self.table, self.in_dtype, zero_init=not self.prior_waves)
+        lib = self.ctx._lib
+        if exchange == "scatter":
+            self._plan_finalize([float(w) for w in total_weights])
+            _native.check(lib.fedavg_sharded_round_scatter(comm.handle, self.ctx._h, self._partial_plan._h,
+                                                           self._finalize_plan._h, chunks, root, self.ctx.stream))
+            return
         fin = None
         if comm.rank == root:
             self.set_accumulated(total_weights)
             fin = self._finalize_plan._h
-        _native.check(self.ctx._lib.fedavg_sharded_round(comm.handle, self.ctx._h, self._partial_plan._h, fin,
-                                                         chunks, root, self.ctx.stream))
+        _native.check(lib.fedavg_sharded_round(comm.handle, self.ctx._h, self._partial_plan._h, fin,
+                                               chunks, root, self.ctx.stream))
+
+    # -- scatter exchange pieces (host-driven path) -----------------------------------------
+    def result_buffer(self) -> torch.Tensor:
+        if self._res is None or self._res.dtype != self.out_dtype:
+            self._res = torch.empty(self.ctx.acc_numel, dtype=self.out_dtype, device=self.ctx.device)
+        return self._res
+
+    def finalize_window(self, src: torch.Tensor, lo: int, hi: int, res: torch.Tensor) -> None:
+        assert self._finalize_plan is not None, "set_accumulated first"
+        self._finalize_plan.finalize_window(src, lo, hi, res)
+
+    def copy_out(self, res: torch.Tensor) -> None:
+        assert self._finalize_plan is not None, "set_accumulated first"
+        self._finalize_plan.copy_out(res)
+
+    def raise_on_nan(self) -> None:
+        """The reference's NaN assertions (fed_avg_algorithm.py:35,93,97) on this rank's flags."""
+        self.ctx.raise_on_nan([(t, self.in_dtype) for t in [*self.prior_waves, self.table] if t is not None])
 
     def fused(self) -> None:
         """Single-rank shortcut: fold + divide in the last wave's launch, no extra fp64 pass."""
@@ -207,6 +274,8 @@ def sharded_reduce(
     global_total_weights: Sequence[float] | None = None,
     force_collective: bool = False,
     comm: RcclComm | None = None,
+    exchange: str = "auto",
+    check_nan: bool = True,
 ) -> list[float]:
     """One FedAvg reduce over every rank's shard; the result lands in the root's outputs.
 
@@ -217,23 +286,43 @@ def sharded_reduce(
     one-rank world the fused single-launch kernel is used (no fp64 round trip) unless
     ``force_collective`` (tests / measurement of the sharded path on one GPU). With ``comm``
     (the library's own RCCL communicator) a HIP reducer runs the whole round in one native call
-    (``fedavg_sharded_round``); otherwise the chunks' reduces go through ``torch.distributed``.
+    (``fedavg_sharded_round[_scatter]``); otherwise the exchange goes through
+    ``torch.distributed``. ``root`` is a rank of ``group``. With ``check_nan`` the root raises
+    the reference's NaN assertions (fed_avg_algorithm.py:35,93,97) before returning; under the
+    scatter exchange another rank's failed window reaches the root as a result NaN.
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1 and not (force_collective and dist.is_initialized()):
         reducer.fused()
+        if check_nan:
+            reducer.raise_on_nan()
         return list(local_total_weights)
     rank = dist.get_rank(group)
+    # torch.distributed addresses the root by its global rank (RcclComm takes the group rank)
+    root_global = dist.get_global_rank(group, root) if group is not None else root
+    acc = reducer.accumulator
+    host_staged = acc.is_cuda and dist.get_backend(group) == "gloo"  # gloo reduces host memory
     if global_total_weights is None:
         totals = torch.tensor([float(w) for w in local_total_weights], dtype=torch.float64,
-                              device=reducer.accumulator.device)
+                              device="cpu" if host_staged or not acc.is_cuda else acc.device)
         dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
         global_total_weights = totals.tolist()
     global_totals = [float(w) for w in global_total_weights]
+    mode = resolve_exchange(exchange, world)
     reducer.prefold()
     if comm is not None and hasattr(reducer, "native_round"):
-        reducer.native_round(comm, global_totals, chunks, root)
-        return global_totals
+        reducer.native_round(comm, global_totals, chunks, root, exchange=mode)
+    elif mode == "scatter":
+        _scatter_exchange(reducer, global_totals, chunks, world, rank, root, root_global, group, host_staged)
+    else:
+        _reduce_exchange(reducer, global_totals, chunks, rank, root, root_global, group, host_staged)
+    if check_nan and rank == root:
+        reducer.raise_on_nan()
+    return global_totals
+
+
+def _reduce_exchange(reducer: LocalReducer, global_totals: list[float], chunks: int, rank: int, root: int,
+                     root_global: int, group: dist.ProcessGroup | None, host_staged: bool) -> None:
     bounds = chunk_bounds(reducer.num_tiles, chunks)
     acc = reducer.accumulator
     # Each chunk's reduce is issued right after its partial kernel, from the compute stream:
@@ -246,7 +335,13 @@ def sharded_reduce(
     for tb, te in bounds:
         reducer.partial(tb, te)
         a, b = reducer.tile_range(tb, te)
-        works.append(dist.reduce(acc[a:b], dst=root, op=dist.ReduceOp.SUM, group=group, async_op=True))
+        if host_staged:
+            h = acc[a:b].cpu()
+            dist.reduce(h, dst=root_global, op=dist.ReduceOp.SUM, group=group)
+            if rank == root:
+                acc[a:b].copy_(h)
+        else:
+            works.append(dist.reduce(acc[a:b], dst=root_global, op=dist.ReduceOp.SUM, group=group, async_op=True))
     # The collectives of one process group run on one RCCL stream and complete in issue
     # order, so on the GPU one wait (the last reduce) covers every chunk: one cross-stream
     # dependency instead of one per chunk. Host backends (gloo) wait for each work.
@@ -255,4 +350,53 @@ def sharded_reduce(
     if rank == root:
         reducer.set_accumulated(global_totals)
         reducer.finalize_range(0, reducer.num_tiles)  # one launch over every tile
-    return global_totals
+
+
+def scatter_windows(a: int, b: int, world: int) -> tuple[int, int]:
+    """Chunk [a, b) of the accumulator -> (L, R): rank r owns [a + r*L, a + (r+1)*L), the
+    R-element tail [a + world*L, b) is reduced to the root (R = 0 whenever world divides 32)."""
+    return divmod(b - a, world)
+
+
+def _scatter_exchange(reducer: LocalReducer, global_totals: list[float], chunks: int, world: int, rank: int,
+                      root: int, root_global: int, group: dist.ProcessGroup | None, host_staged: bool) -> None:
+    """Host-driven form of fedavg_sharded_round_scatter (same windows, same arithmetic)."""
+    bounds = chunk_bounds(reducer.num_tiles, chunks)
+    acc = reducer.accumulator
+    reducer.set_accumulated(global_totals)  # every rank divides its own windows
+    res = reducer.result_buffer()
+    for tb, te in bounds:
+        reducer.partial(tb, te)
+        a, b = reducer.tile_range(tb, te)
+        L, R = scatter_windows(a, b, world)
+        lo = a + rank * L
+        if L > 0:
+            src = acc[a : a + world * L]
+            if host_staged:
+                mine = torch.empty(L, dtype=torch.float64)
+                dist.reduce_scatter_tensor(mine, src.cpu(), op=dist.ReduceOp.SUM, group=group)
+                mine = mine.to(acc.device)
+            else:
+                mine = torch.empty(L, dtype=torch.float64, device=acc.device)
+                dist.reduce_scatter_tensor(mine, src, op=dist.ReduceOp.SUM, group=group)
+            reducer.finalize_window(mine, lo, lo + L, res)
+        if R > 0:
+            tail = acc[a + world * L : b]
+            h = tail.cpu() if host_staged else tail
+            dist.reduce(h, dst=root_global, op=dist.ReduceOp.SUM, group=group)
+            if rank == root:
+                reducer.finalize_window(h.to(acc.device) if host_staged else tail, a + world * L, b, res)
+        if L > 0:
+            send = res[lo : lo + L]
+            if host_staged:
+                recv = [torch.empty(L, dtype=res.dtype) for _ in range(world)] if rank == root else None
+                dist.gather(send.cpu(), recv, dst=root_global, group=group)
+                if rank == root:
+                    for i, t in enumerate(recv):
+                        if i != root:
+                            res[a + i * L : a + (i + 1) * L].copy_(t)
+            else:
+                recv = [res[a + i * L : a + (i + 1) * L] for i in range(world)] if rank == root else None
+                dist.gather(send, recv, dst=root_global, group=group)
+    if rank == root:
+        reducer.copy_out(res)

@@ -94,6 +94,14 @@ typedef struct fedavg_ctx fedavg_ctx;
 
 int32_t fedavg_abi_version(void);
 
+/* Compile-time variants the library was built with: 0 for the product build. Non-zero bits
+ * mark timing-only ablation builds whose results are WRONG by design (kernel A/B studies):
+ * FEDAVG_BUILD_ABLATE_EPILOGUE (reciprocal multiply, no NaN checks), FEDAVG_BUILD_ABLATE_QSGD.
+ * Bindings refuse to load such a build unless asked to (_native.py). */
+#define FEDAVG_BUILD_ABLATE_EPILOGUE 0x1
+#define FEDAVG_BUILD_ABLATE_QSGD 0x2
+int32_t fedavg_build_flags(void);
+
 /* Byte size of one QSGD record of a numel-element tensor, and the offset of its sign bits
  * (see FEDAVG_QSGD_F32). Pure functions; -1 for numel < 0. */
 int64_t fedavg_qsgd_record_bytes(int64_t numel);
@@ -107,8 +115,13 @@ const char* fedavg_last_error(void);
  *               (e.g. a torch tensor, so a collective can run on it); NULL = the context
  *               allocates its own.
  * The fp64 accumulator uses a padded flat layout: segment t starts at
- * fedavg_segment_offset(ctx, t) (a multiple of 2 elements = 16 bytes).
+ * fedavg_segment_offset(ctx, t), a multiple of FEDAVG_ACC_ALIGN elements (256 bytes: every
+ * tile boundary in accumulator coordinates is then divisible by 32, so the scatter exchange of
+ * the multi-GPU round splits a chunk evenly over 2 / 4 / 8 ranks with 16-B aligned windows).
+ * fedavg_layout_acc_numel gives the size before a context exists (for caller-owned buffers).
  */
+#define FEDAVG_ACC_ALIGN 32
+int64_t fedavg_layout_acc_numel(const int64_t* seg_numel, int32_t num_segments);
 int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_numel,
                           int32_t num_segments, void* accumulator);
 int32_t fedavg_ctx_destroy(fedavg_ctx* ctx);
@@ -234,6 +247,18 @@ int32_t fedavg_plan_create_finalize(fedavg_ctx* ctx, const double* total_weights
                                     void* const* out_ptrs, int32_t out_dtype, fedavg_plan** out);
 int32_t fedavg_plan_run_range(fedavg_plan* plan, int32_t tile_begin, int32_t tile_end, void* stream);
 
+/* Pieces of the scatter exchange (fedavg_sharded_round_scatter; also usable from a host-driven
+ * exchange, sharded.py). `finalize` is a finalize plan (its totals, outputs and out dtype).
+ *  fedavg_plan_finalize_window: res[p] = src[p - lo] / W[seg(p)] for accumulator positions p in
+ *      [lo, hi) that belong to a segment (padding is skipped); res is a buffer of the plan's out
+ *      dtype in accumulator coordinates (fedavg_acc_numel elements); NaN checks as finalize.
+ *  fedavg_plan_copy_out: the plan's outputs <- res (accumulator coordinates), every tile; a NaN
+ *      in res raises the result flag (another rank's failed window reaches the root's check). */
+int32_t fedavg_plan_finalize_window(fedavg_plan* finalize, const double* src, int64_t lo, int64_t hi, void* res,
+                                    void* stream);
+int32_t fedavg_plan_copy_out(fedavg_plan* finalize, const void* res, void* stream);
+int32_t fedavg_plan_out_dtype(const fedavg_plan* plan); /* FEDAVG_F32 / FEDAVG_F64; -1 if none */
+
 /*
  * Synchronise `stream` and report the NaN flag: FEDAVG_OK, FEDAVG_ERR_NAN_ACCUM or
  * FEDAVG_ERR_NAN_RESULT. *flags_out (optional) receives the raw flag bits.
@@ -333,6 +358,22 @@ int32_t fedavg_comm_create(fedavg_comm** out, const void* id, int32_t world, int
 int32_t fedavg_comm_destroy(fedavg_comm* comm);
 int32_t fedavg_sharded_round(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
                              int32_t chunks, int32_t root, void* stream);
+/*
+ * The same round with a scatter exchange instead of a reduce to the root (DESIGN.md §5 cost
+ * table). Every rank passes a finalize plan (non-root ranks: scratch outputs of the same
+ * layout). Per chunk [A, B) of the accumulator (B - A = G*L + R):
+ *   ncclReduceScatter of acc[A, A + G*L) (rank r receives the sums of window
+ *   [A + r*L, A + (r+1)*L)) — plus, when R > 0, an ncclReduce of the R-element tail to the root,
+ *   in one group — on the comm stream behind the chunk's partial kernel; each rank divides its
+ *   window (fedavg_plan_finalize_window) and ncclGather collects the windows, in the output dtype,
+ *   into the root's result buffer (accumulator coordinates). `stream` then waits for the last
+ *   gather and the root copies the result into its outputs (fedavg_plan_copy_out). A NaN on any
+ *   rank's window surfaces in the root's fedavg_check (as FEDAVG_ERR_NAN_RESULT).
+ * Root ingress: (G-1)/G of the fp64 partial + (G-1)/G of the result, against the whole fp64
+ * partial for fedavg_sharded_round; every rank egresses the same (G-1)/G of its partial.
+ */
+int32_t fedavg_sharded_round_scatter(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* partial,
+                                     fedavg_plan* finalize, int32_t chunks, int32_t root, void* stream);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,38 @@ class RefOpsFedAvg:
         return out
 
 
+class RefFedAvgAlgorithm:
+    """The reference's FedAVGAlgorithm call sequence (fed_avg_algorithm.py:20-113) over message
+    objects, in the reference's torch CPU ops: ``process_worker_data`` per arrival (NaN assert,
+    weighted fp64 fold, payload released, :20-64), ``aggregate_worker_data`` at the end (NaN
+    asserts, divide, other_data check, first-arrival flags, :76-113). bench.py's cpu_baseline
+    times process_worker_data x N + aggregate_worker_data on pre-built messages."""
+
+    def __init__(self) -> None:
+        self.ops = RefOpsFedAvg()
+        self.all_worker_data: dict = {}
+
+    def process_worker_data(self, worker_id: int, worker_data) -> bool:
+        self.all_worker_data[worker_id] = worker_data
+        if worker_data is None:
+            return True
+        self.ops.add(worker_data.parameter, worker_data.aggregation_weight)
+        worker_data.parameter = {}  # :63-64
+        return True
+
+    def aggregate_worker_data(self) -> dict:
+        parameter = self.ops.finish()
+        other: dict = {}
+        for msg in self.all_worker_data.values():
+            for k, v in msg.other_data.items():
+                if k in other and other[k] != v:
+                    raise RuntimeError(f"different values on key {k}")
+                other.setdefault(k, v)
+        first = next(iter(self.all_worker_data.values()))
+        return {"parameter": parameter, "other_data": other, "in_round": first.in_round,
+                "end_training": first.end_training}
+
+
 class RefOpsPersonalized:
     """The reference's PersonalizedFedAVG op sequence (personalized_aggregation_algorithm.py:23-57)
     in torch CPU ops, for bench.py's personalized cpu_baseline: every arrival is deep-copied into

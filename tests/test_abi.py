@@ -39,3 +39,19 @@ def test_null_context_is_rejected_without_a_gpu():
     lib = _native.load()
     assert lib.fedavg_reset(None, None) == _native.ERR_INVALID
     assert "null context" in _native.last_error()
+
+
+def test_product_build_is_not_an_ablation_build():
+    lib = _native.load()
+    assert lib.fedavg_build_flags() == 0
+
+
+def test_layout_acc_numel_aligns_segments():
+    import ctypes
+
+    lib = _native.load()
+    numels = [1, 31, 32, 33, 4097]
+    arr = (ctypes.c_int64 * len(numels))(*numels)
+    want = sum((n + _native.ACC_ALIGN - 1) // _native.ACC_ALIGN * _native.ACC_ALIGN for n in numels)
+    assert lib.fedavg_layout_acc_numel(arr, len(numels)) == want
+    assert lib.fedavg_layout_acc_numel(arr, 0) == -1

@@ -1,7 +1,8 @@
 """Multi-rank FedAvg (clients sharded over ranks + chunked reduce) on CPU with gloo.
 
-Covers ``sharded.sharded_reduce`` — chunking, the reduce of fp64 partials to the root, the
-weight totals and the per-chunk finalize — with world_size 2 and 3 on the CPU. The per-rank
+Covers ``sharded.sharded_reduce`` — chunking, both exchanges (the reduce of fp64 partials to
+the root; the reduce-scatter + window finalize + gather), the weight totals, the root's NaN
+check, sub-groups — with world_size 2 and 3 on the CPU. The per-rank
 compute is a plain torch stand-in for the HIP reducer (same tile geometry as the native
 library: 2048-element tiles that never cross a tensor, 16-byte aligned accumulator
 segments); the GPU parity tests cover the HIP reducer itself.
@@ -67,6 +68,30 @@ class TorchCPUReducer:
     def prefold(self):
         pass
 
+    # scatter exchange pieces: a window of accumulator positions, padding skipped
+    def _seg_of(self):
+        seg = torch.full((self.accumulator.numel(),), -1, dtype=torch.int64)
+        for s_, (o, n) in enumerate(zip(self.acc_off, self.layout.numels)):
+            seg[o : o + n] = s_
+        return seg
+
+    def result_buffer(self):
+        return torch.full((self.accumulator.numel(),), float("nan"), dtype=torch.float64)
+
+    def finalize_window(self, src, lo, hi, res):
+        seg = self._seg_of()[lo:hi]
+        keep = seg >= 0
+        tot = torch.tensor(self.totals, dtype=torch.float64)
+        res[lo:hi][keep] = src[: hi - lo][keep] / tot[seg[keep]]
+
+    def copy_out(self, res):
+        for s_, (o, n) in enumerate(zip(self.acc_off, self.layout.numels)):
+            self.outs[s_][:] = res[o : o + n]
+
+    def raise_on_nan(self):
+        if self.outs is not None:
+            assert not any(bool(o.isnan().any()) for o in self.outs), "NaN in the aggregate"
+
     def fused(self):
         self.partial(0, self.num_tiles)
         self.set_accumulated([sum(w[s] for w in self.weights) for s in range(self.layout.num_segments)])
@@ -84,18 +109,25 @@ def make_all_clients(n):
     return clients, weights
 
 
-def _worker(rank, world, port, n_clients, chunks, pass_totals, q):
+def _worker(rank, world, port, n_clients, chunks, pass_totals, q, exchange="reduce", subgroup=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        group = None
+        if subgroup:  # the shard ranks are global ranks 1..world-1; group rank 0 = global rank 1
+            group = dist.new_group(list(range(1, world)))
+            if rank == 0:
+                return
+        g_world, g_rank = dist.get_world_size(group), dist.get_rank(group)
         clients, weights = make_all_clients(n_clients)
-        mine = [i for i in range(n_clients) if i % world == rank]
-        outs = [torch.empty(m, dtype=torch.float64) for m in LAYOUT.numels] if rank == 0 else None
+        mine = [i for i in range(n_clients) if i % g_world == g_rank]
+        outs = [torch.empty(m, dtype=torch.float64) for m in LAYOUT.numels] if g_rank == 0 else None
         red = TorchCPUReducer(LAYOUT, [clients[i] for i in mine], [weights[i] for i in mine], outs)
         local = [sum(weights[i][s] for i in mine) for s in range(LAYOUT.num_segments)]
         glob = [sum(w[s] for w in weights) for s in range(LAYOUT.num_segments)] if pass_totals else None
-        totals = sharded_reduce(red, local, chunks=chunks, global_total_weights=glob)
-        if rank == 0:
+        totals = sharded_reduce(red, local, chunks=chunks, global_total_weights=glob, group=group,
+                                exchange=exchange)
+        if g_rank == 0:
             q.put(("ok", [o.numpy() for o in outs], totals))
     except Exception as e:  # pragma: no cover - surfaced by the parent
         q.put(("err", repr(e), None))
@@ -110,13 +142,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,chunks,pass_totals", [(2, 4, True), (2, 1, False), (3, 3, False)])
-def test_sharded_reduce_gloo(world, chunks, pass_totals):
+@pytest.mark.parametrize("exchange", ["reduce", "scatter"])
+@pytest.mark.parametrize("world,chunks,pass_totals,subgroup", [(2, 4, True, False), (2, 1, False, False),
+                                                               (3, 3, False, False), (3, 2, True, True)])
+def test_sharded_reduce_gloo(world, chunks, pass_totals, subgroup, exchange):
     n_clients = 7
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_clients, chunks, pass_totals, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_clients, chunks, pass_totals, q, exchange, subgroup))
+             for r in range(world)]
     for p in procs:
         p.start()
     status, outs, totals = q.get(timeout=120)
@@ -143,6 +178,52 @@ def test_single_rank_uses_the_fused_path():
     for s in range(4):
         want = fedavg_flat([c[s].numpy() for c in clients], [w[s] for w in weights])
         np.testing.assert_allclose(outs[s].numpy(), want, rtol=1e-14)
+
+
+def _nan_worker(rank, world, port, exchange, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        clients, weights = make_all_clients(4)
+        if rank == world - 1:
+            clients[rank][2][100] = float("nan")  # the last rank's shard holds a NaN
+        mine = [i for i in range(4) if i % world == rank]
+        outs = [torch.empty(m, dtype=torch.float64) for m in LAYOUT.numels] if rank == 0 else None
+        red = TorchCPUReducer(LAYOUT, [clients[i] for i in mine], [weights[i] for i in mine], outs)
+        local = [sum(weights[i][s] for i in mine) for s in range(LAYOUT.num_segments)]
+        try:
+            sharded_reduce(red, local, chunks=2, exchange=exchange)
+            q.put((rank, "no error"))
+        except AssertionError:
+            q.put((rank, "AssertionError"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("exchange", ["reduce", "scatter"])
+def test_root_raises_on_a_nan_in_another_shard(exchange):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_nan_worker, args=(r, world, port, exchange, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert got[0] == "AssertionError"  # the root sees the NaN (fed_avg_algorithm.py:35/93/97)
+
+
+def test_resolve_exchange():
+    from distributed_learning_simulation_lib_amd.sharded import resolve_exchange, scatter_windows
+
+    assert resolve_exchange("auto", 2) == "scatter" and resolve_exchange("auto", 4) == "reduce"
+    assert resolve_exchange("reduce", 2) == "reduce"
+    with pytest.raises(ValueError):
+        resolve_exchange("allreduce", 2)
+    assert scatter_windows(64, 64 + 4096 * 3, 8) == (4096 * 3 // 8, 0)
+    assert scatter_windows(0, 10, 3) == (3, 1)
 
 
 def test_chunk_bounds_partition_tiles():

@@ -641,8 +641,10 @@ def main() -> int:
         # rank 0 ends the round on the host: sharded_reduce reads the NaN flags there (the
         # reference's assertions, fed_avg_algorithm.py:35,93,97)
         sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals,
-                       force_collective=args.force_collective, comm=comm, exchange=exchange)
+                       force_collective=args.force_collective, comm=comm, exchange=exchange, check_nan=False)
         host_enqueue[0] += time.perf_counter() - h0
+        if rank == 0:
+            reducer.raise_on_nan()
 
     for _ in range(args.warmup):
         step()

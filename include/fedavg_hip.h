@@ -201,7 +201,9 @@ int32_t fedavg_weighted_avg(fedavg_ctx* ctx, const void* const* client_ptrs, int
 
 /*
  * Multi-GPU shard step: acc[tiles in [tile_begin, tile_end)] = (acc_in ? acc : 0) +
- * sum_k w_k x_k, fp64, written to the accumulator (no division). Used by the sharded
+ * sum_k w_k x_k, fp64, written to the accumulator (no division); acc_in = the context holds
+ * accumulated data for the segment (earlier waves through fedavg_accumulate, or
+ * fedavg_set_accumulated) and zero_init == 0. Used by the sharded
  * driver that reduces the per-GPU partials with RCCL and then calls fedavg_aggregate
  * with num_clients = 0 on the root. tile_end = -1 means "all tiles". zero_init != 0 starts
  * every segment at the additive identity -0.0 (so the shard's fold is exact, and a shard

@@ -24,6 +24,7 @@ import torch
 
 from bench import dataset_size_weights, gpt2s_layout, resnet18_layout
 from distributed_learning_simulation_lib_amd.fedavg import ClientTable, FedAvgContext
+from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer
 
 pytestmark = pytest.mark.gpu
 
@@ -62,12 +63,18 @@ def _run_sharded(layout, dtype, n_total, shards, wave, hip_device):
     for r in range(shards):
         torch.cuda.synchronize(hip_device)  # the previous shard's kernels are done with the buffer
         _fill(buckets, r * per)
+        tables = []
         for w0 in range(0, per, wave):
             table = ClientTable(T)
             for k in range(w0, min(per, w0 + wave)):
                 row = [buckets[k, o : o + m] for o, m in zip(offs, layout.numels)]
                 table.add_client(row, [weights[r * per + k]] * T)
-            ctx.partial(table, dtype, zero_init=(w0 == 0))
+            tables.append(table)
+        # the rank's reducer: earlier waves folded into the accumulator, the last one as the
+        # (chunkable) partial continuing from it
+        red = HipLocalReducer(ctx, tables[-1], dtype, None, torch.float32, prior_waves=tables[:-1])
+        red.prefold()
+        red.partial(0, ctx.num_tiles)
         summed += ctx.accumulator  # rank-order sum of the shard partials (the reduce)
         xs[r * per : (r + 1) * per] = buckets[:, bucket_idx].double().cpu().numpy()
     ctx.accumulator.copy_(summed)

@@ -98,6 +98,10 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_plan_create_finalize": (c_int32, [c_void_p, _PD, _PP, c_int32, POINTER(c_void_p)]),
     "fedavg_plan_run_range": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_plan_destroy": (c_int32, [c_void_p]),
+    "fedavg_set_segment_state": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
+    "fedavg_accumulate_elementwise": (
+        c_int32, [c_void_p, _PP, c_int32, _PP, POINTER(c_int32), _PD, POINTER(c_int32), c_int32, c_void_p, c_void_p]),
+    "fedavg_finalize_elementwise": (c_int32, [c_void_p, c_void_p, _PP, c_int32, c_void_p]),
     "fedavg_plan_finalize_window": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "fedavg_plan_copy_out": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "fedavg_plan_out_dtype": (c_int32, [c_void_p]),

@@ -15,12 +15,22 @@ rounded products and sums — bit-identical to the reference's fp64 sequence. Th
 folded and divided by the total weight in the same launch (``fedavg_aggregate``), with the
 reference's NaN assertions fused into the kernel.
 
+The hooks keep the reference's full semantics (golden cases in tests/golden, generated from the
+reference's own code):
+  * ``_get_weight`` may return a number, a 0-dim tensor — whose total then accumulates in the
+    tensor's dtype through the reference's ``total += weight`` (:59-62, reproduced on the host
+    with the very same objects) — or a tensor of the parameter's shape (per-element weights:
+    ``fedavg_accumulate_elementwise`` keeps a per-element total on the GPU);
+  * ``_apply_total_weight`` overridden by a subclass receives the fp64 weighted sum and the
+    same total object the reference would pass;
+  * a tensor name that first appears in a later client grows the layout (:55-62), keeping the
+    accumulated state; output keys come in first-seen order.
+
 Differences a caller can observe, all documented in DESIGN.md:
-  * the NaN assertions fire at the wave flush / aggregate, not at the offending arrival;
+  * the NaN assertion on an arriving update (:35) fires at the wave flush / aggregate unless
+    ``eager_nan_check`` (or ``FEDAVG_EAGER_NAN=1``) scans every arrival on the GPU first;
   * ``aggregate_worker_data`` returns float64 tensors on the GPU (``result_device`` moves
-    them, e.g. to ``"cpu"`` as the reference's server does on caching);
-  * a key that first appears in a later client than the first one raises
-    ``NotImplementedError`` (the reference server always calls ``complete()`` first).
+    them, e.g. to ``"cpu"`` as the reference's server does on caching).
 """
 
 from __future__ import annotations
@@ -29,6 +39,7 @@ import os
 from collections.abc import MutableMapping
 from typing import Any
 
+import numpy as np
 import torch
 
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
@@ -52,6 +63,30 @@ from .aggregation_algorithm import (
 )
 
 
+def _is_elementwise(weight: Any, parameter: Any) -> bool:
+    """A _get_weight value that is a tensor of the parameter's shape (not a scalar)."""
+    if isinstance(weight, torch.Tensor) and weight.numel() != 1:
+        if isinstance(parameter, torch.Tensor) and tuple(weight.shape) == tuple(parameter.shape):
+            return True
+        raise NotImplementedError(
+            f"a _get_weight tensor of shape {tuple(weight.shape)} for a parameter of shape "
+            f"{tuple(getattr(parameter, 'shape', ()))}: scalars and per-element weights are supported"
+        )
+    if isinstance(weight, np.ndarray) and weight.size != 1:
+        raise NotImplementedError("per-element weights must be torch tensors")
+    return False
+
+
+def _total_is_fp32(weight: Any) -> bool:
+    """The reference's `total = weight; total += ...` keeps the first weight's dtype."""
+    dt = getattr(weight, "dtype", None)
+    if dt in (torch.float32, np.float32):
+        return True
+    if dt in (torch.float16, torch.bfloat16, np.float16):
+        raise NotImplementedError("fp16 / bf16 weight tensors are not supported (fp32 / fp64 / numbers are)")
+    return False
+
+
 class FedAVGAlgorithm(AggregationAlgorithm):
     def __init__(
         self,
@@ -60,6 +95,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         result_dtype: torch.dtype = torch.float64,
         result_device: torch.device | str | None = None,
         split_policy: int = 1,
+        eager_nan_check: bool | None = None,
     ) -> None:
         super().__init__()
         self.accumulate: bool = True
@@ -70,6 +106,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.result_dtype = result_dtype
         self.result_device = torch.device(result_device) if result_device is not None else None
         self.split_policy = split_policy
+        # the reference asserts each arriving tensor is NaN-free (fed_avg_algorithm.py:34-35);
+        # by default the fused flags report it at the wave flush, eagerly on request
+        self.eager_nan_check = (os.environ.get("FEDAVG_EAGER_NAN") == "1") if eager_nan_check is None \
+            else bool(eager_nan_check)
         self.__layout: ModelLayout | None = None
         self.__native_layout: ModelLayout | None = None
         self.__keep: list[int] = []
@@ -84,6 +124,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__ingest: HostIngest | None = None
         self.__result_flat: torch.Tensor | None = None
         self.__record_layouts: dict[tuple[int, ...], ModelLayout] = {}
+        # fed_avg_algorithm.py:59-62, kept with the hook's own objects (scalar weights)
+        self.__host_totals: dict[str, Any] = {}
+        # per-element weights: decided by the round's first update
+        self.__ew: bool | None = None
+        self.__tot_fp32: dict[str, bool] = {}
+        self.__ew_totals: torch.Tensor | None = None
 
     # ---- setup -------------------------------------------------------------------------
     @property
@@ -100,11 +146,43 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 self.__ctx.close()
             self.__ctx = FedAvgContext(self.__native_layout, self.device, split_policy=self.split_policy)
             self.__ctx_key = key
+            self.__ew_totals = None
         return self.__ctx
 
     def _set_layout(self, parameter: ModelParameter) -> None:
         self.__layout = ModelLayout.from_parameters(parameter)
         self.__native_layout, self.__keep = split_empty(self.__layout)
+
+    def _grow_layout(self, unknown: list[str], row: dict[str, tuple[Any, Any]]) -> None:
+        """Names first seen in a later client (fed_avg_algorithm.py:55-62): append them to the
+        layout, moving what is accumulated so far into a context of the grown layout."""
+        self._flush()
+        old_layout, old_native, old_ctx = self.__layout, self.__native_layout, self.__ctx
+        assert old_layout is not None
+        # what the old context holds, read before it is replaced
+        old_state = None
+        if old_ctx is not None and old_native is not None:
+            old_state = ([old_ctx.segment_offset(j) for j in range(old_native.num_segments)],
+                         old_ctx.total_weights(), old_ctx.accumulator, self.__ew_totals)
+        self.__layout = ModelLayout(names=old_layout.names + tuple(unknown),
+                                    shapes=old_layout.shapes + tuple(tuple(row[k][0].shape) for k in unknown))
+        self.__native_layout, self.__keep = split_empty(self.__layout)
+        self.__base = None
+        if old_state is None or self.__native_layout is None:
+            return
+        old_offs, old_totals, old_acc, old_ew = old_state
+        new_ctx = self._context()  # closes the old context
+        index = {n: i for i, n in enumerate(self.__native_layout.names)}
+        totals = [0.0] * self.__native_layout.num_segments
+        valid = [0] * self.__native_layout.num_segments
+        for j, (name, n) in enumerate(zip(old_native.names, old_native.numels)):
+            k = index[name]
+            src, dst = old_offs[j], new_ctx.segment_offset(k)
+            new_ctx.accumulator[dst : dst + n].copy_(old_acc[src : src + n])
+            if old_ew is not None:
+                self._ew_totals_buffer()[dst : dst + n].copy_(old_ew[src : src + n])
+            totals[k], valid[k] = old_totals[j], 1
+        new_ctx.set_segment_state(totals, valid)
 
     # ---- per arrival (fed_avg_algorithm.py:20-41) --------------------------------------
     def process_worker_data(
@@ -120,34 +198,45 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             return True
         # messages are recognised by their dataclass fields, not by class identity: the
         # reference's own server passes simulation_lib.message objects (message.py)
-        if is_delta_message(worker_data) and not (self.accumulate and self._delta_fusable(worker_data)):
-            # a delta the fold cannot take (consistency-check fields, or the ratio path keeps
-            # whole updates): restore it on the host exactly as the reference server does
-            # (aggregation_server.py:123-125) and keep the full update in its place
-            assert self._old_parameter is not None, "a delta update needs the cached global model"
-            worker_data = worker_data.restore(self._old_parameter)
-            self._all_worker_data[worker_id] = worker_data
+        if is_delta_message(worker_data) and not (self.accumulate and self._delta_fusable(worker_data)
+                                                  and not self.__ew):
+            worker_data = self._restore_on_host(worker_id, worker_data)
         if is_delta_message(worker_data):
             # restore() fused into the fold: x = old + delta in the kernel (message.py:40-61)
             assert self._old_parameter is not None
             assert len(worker_data.delta_parameter) == len(self._old_parameter)
             if self.__layout is None:
                 self._set_layout(self._old_parameter)
-            self.__row = {}
+            row = {}
             for name, delta in worker_data.delta_parameter.items():
-                weight = self._get_weight(worker_data=worker_data, name=name, parameter=delta)
-                self.__row[name] = (delta, weight)
-            worker_data.delta_parameter = {}
-            self._stage_client(delta=True)
-            return True
+                row[name] = (delta, self._get_weight(worker_data=worker_data, name=name, parameter=delta))
+            if any(_is_elementwise(w, t) for t, w in row.values()):
+                # per-element weights take the dense elementwise fold: restore first
+                worker_data = self._restore_on_host(worker_id, worker_data)
+            else:
+                for name, (delta, weight) in row.items():
+                    self._note_total(name, weight, delta)
+                self.__row = row
+                worker_data.delta_parameter = {}
+                self._stage_client(delta=True, worker_id=worker_id)
+                return True
         if not is_parameter_message(worker_data):
             return True
         self.__row = {}
         for name, parameter in worker_data.parameter.items():
             self._accumulate_parameter(worker_data=worker_data, name=name, parameter=parameter)
         if self.accumulate:
-            self._stage_client()
+            self._stage_client(worker_id=worker_id)
         return True
+
+    def _restore_on_host(self, worker_id: int, worker_data: Any) -> Any:
+        """A delta the fold cannot take (consistency-check fields, the ratio path, per-element
+        weights): restore it with its own restore() exactly as the reference server does
+        (aggregation_server.py:123-125) and keep the full update in its place."""
+        assert self._old_parameter is not None, "a delta update needs the cached global model"
+        restored = worker_data.restore(self._old_parameter)
+        self._all_worker_data[worker_id] = restored
+        return restored
 
     # The server hands DeltaParameterMessages straight to this algorithm (with the cached global
     # model set through set_old_parameter) instead of restoring them on the host first.
@@ -182,10 +271,21 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if not self.accumulate:
             return
         weight = self._get_weight(worker_data=worker_data, name=name, parameter=parameter)
+        self._note_total(name, weight, parameter)
         # host tensors are packed and DMA'd per client in _stage_client (ingest.HostIngest)
         self.__row[name] = (parameter, weight)
         # release to reduce memory pressure (fed_avg_algorithm.py:63-64)
         worker_data.parameter = {}
+
+    def _note_total(self, name: str, weight: Any, parameter: Any) -> None:
+        """fed_avg_algorithm.py:59-62 with the hook's own objects (a 0-dim tensor total stays a
+        tensor of its dtype, updated in place). Per-element totals live on the GPU instead."""
+        if _is_elementwise(weight, parameter):
+            return
+        if name not in self.__host_totals:
+            self.__host_totals[name] = weight
+        else:
+            self.__host_totals[name] += weight
 
     def _get_weight(self, worker_data: ParameterMessage, name: str, parameter: Any) -> Any:
         return worker_data.aggregation_weight
@@ -193,7 +293,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _apply_total_weight(self, name: str, parameter: torch.Tensor, total_weight: Any) -> torch.Tensor:
         return parameter / total_weight
 
-    def _stage_client(self, delta: bool = False) -> None:
+    def _stage_client(self, delta: bool = False, worker_id: int | None = None) -> None:
         row = self.__row
         self.__row = {}
         if not row:
@@ -201,17 +301,26 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if self.__layout is None:
             self._set_layout({k: v[0] for k, v in row.items()})
         assert self.__layout is not None
-        unknown = [k for k in row if k not in self.__layout.names]
+        known = set(self.__layout.names)
+        unknown = [k for k in row if k not in known]
         if unknown:
-            raise NotImplementedError(
-                f"tensors {unknown} were not in the first client's update; complete() the "
-                "message against the global model first (aggregation_server.py:126-128)"
-            )
+            if delta:
+                raise NotImplementedError(f"delta tensors {unknown} are not in the cached global model")
+            self._grow_layout(unknown, row)
         if self.__native_layout is None:
             self.__has_data = True
             return
+        ew_here = any(_is_elementwise(w, t) for t, w in row.values())
+        if self.__ew is None:
+            self.__ew = ew_here
+        elif ew_here and not self.__ew:
+            raise NotImplementedError(
+                "per-element weights must be returned from the round's first update on "
+                "(the reference's scalar total cannot be added in place into a tensor, fed_avg_algorithm.py:62)"
+            )
         tensors: list[torch.Tensor | None] = []
         weights: list[float] = []
+        weight_tensors: list[torch.Tensor | None] = []
         for i in self.__keep:
             name = self.__layout.names[i]
             if name in row:
@@ -220,13 +329,24 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     raise ValueError(f"shape of {name} changed: {tuple(t.shape)} vs {self.__layout.shapes[i]}")
                 assert w is not None, "aggregation_weight is None"
                 tensors.append(t)
+                if self.__ew:
+                    self.__tot_fp32.setdefault(name, _total_is_fp32(w))
+                    if _is_elementwise(w, t):
+                        wt = w.detach().to(device=self.device).contiguous()
+                        if wt.dtype not in (torch.float32, torch.float64):
+                            wt = wt.to(torch.float64)
+                        weight_tensors.append(wt)
+                        weights.append(0.0)
+                        continue
+                weight_tensors.append(None)
                 weights.append(float(w))
             else:
                 tensors.append(None)
                 weights.append(0.0)
+                weight_tensors.append(None)
         present = [t for t in tensors if t is not None]
         codecs = {t.codec for t in present if isinstance(t, QuantizedTensor)}
-        if codecs and len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in present):
+        if codecs and len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in present) and not self.__ew:
             # quantised update: the records are the kernel operands (dequantised in the fold)
             dt = codecs.pop()
             tensors = self._records_to_device(tensors)
@@ -241,16 +361,28 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 tensors = [next(it) if t is not None else None for t in tensors]
             else:
                 dt = self.__table_dtype or torch.float32
+        if self.eager_nan_check:
+            self._scan_arrival(tensors, dt, worker_id, delta)
         if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
             self._flush()
         if self.__table is None:
             self.__table = ClientTable(len(self.__keep))
             self.__table_dtype = dt
             self.__table_delta = delta
-        self.__table.add_client(tensors, weights)
+        self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
         self.__has_data = True
         if self.__table.num_clients >= self.wave_size:
             self._flush()
+
+    def _scan_arrival(self, tensors: list, dt: Any, worker_id: int | None, delta: bool) -> None:
+        """fed_avg_algorithm.py:34-35 at the arrival: one GPU scan of the staged update."""
+        if delta:
+            return  # the delta fold restores first; its NaN surfaces at the flush (:93)
+        t1 = ClientTable(len(tensors))
+        t1.add_client(tensors, [1.0] * len(tensors))
+        if self._context().find_nan_clients(t1, dt):
+            raise NaNAggregationError("input", f"NaN in the update of worker {worker_id} (fed_avg_algorithm.py:35)",
+                                      [worker_id] if worker_id is not None else [])
 
     def _to_device_row(self, tensors: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
         """One client's tensors in HBM. Host tensors of one kernel dtype go through the pinned
@@ -305,6 +437,17 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 out.append(q.record if q.device == self.device else q.record.to(self.device))
         return out
 
+    def _ew_totals_buffer(self) -> torch.Tensor:
+        """Per-element totals (fp64, accumulator coordinates) of the elementwise fold."""
+        ctx = self._context()
+        if self.__ew_totals is None or self.__ew_totals.numel() != ctx.acc_numel:
+            self.__ew_totals = torch.zeros(ctx.acc_numel, dtype=torch.float64, device=self.device)
+        return self.__ew_totals
+
+    def _tot_fp32_flags(self) -> list[bool]:
+        assert self.__native_layout is not None
+        return [self.__tot_fp32.get(n, False) for n in self.__native_layout.names]
+
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""
         if self.__table is None or self.__table.num_clients == 0:
@@ -313,7 +456,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         table, dt = self.__table, self.__table_dtype
         assert dt is not None
         self.__table, self.__table_dtype = None, None
-        if self.__table_delta:
+        if self.__ew:
+            ctx.accumulate_elementwise(table, dt, self._ew_totals_buffer(), self._tot_fp32_flags())
+        elif self.__table_delta:
             ctx.accumulate_delta(table, dt, self._delta_base())
         else:
             ctx.accumulate(table, dt)
@@ -333,16 +478,24 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         layout = self.__layout
         assert layout is not None
         result: ModelParameter = {}
-        if self.__native_layout is not None:
-            result.update(self._finish_native())
+        try:
+            if self.__native_layout is not None:
+                result.update(self._finish_native())
+        finally:
+            self._reset_round()
         for i, name in enumerate(layout.names):
             if i not in self.__keep:
                 result[name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
-        self.__has_data = False
         out = {name: result[name] for name in layout.names}
         if self.result_device is not None:
             out = self._move_result(out)
         return out
+
+    def _reset_round(self) -> None:
+        self.__has_data = False
+        self.__host_totals = {}
+        self.__ew = None
+        self.__tot_fp32 = {}
 
     def _move_result(self, out: ModelParameter) -> ModelParameter:
         """Results to ``result_device``: the native part lives in one flat device buffer, so a
@@ -373,6 +526,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__table, self.__table_dtype = None, None
         pending = [(table, dt)] if table is not None and dt is not None else []
         custom_divide = type(self)._apply_total_weight is not FedAVGAlgorithm._apply_total_weight
+        names = [layout.names[i] for i in self.__keep]
+        # a 0-dim tensor (or other non-number) total: divide by the host total the reference has
+        host_divide = not self.__ew and any(not isinstance(self.__host_totals.get(n, 0), (int, float))
+                                            for n in names)
         out_dtype = torch.float64 if custom_divide else self.result_dtype
         flat = torch.empty(native.padded_offsets(8 if out_dtype == torch.float64 else 4)[1],
                            dtype=out_dtype, device=self.device)
@@ -381,37 +538,69 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         outs = [flat[o : o + n] for o, n in zip(offs, native.numels)]
         delta = self.__table_delta and table is not None
         try:
-            if not custom_divide:
+            if self.__ew:
+                if table is not None and dt is not None:
+                    ctx.accumulate_elementwise(table, dt, self._ew_totals_buffer(), self._tot_fp32_flags())
+                if not custom_divide:
+                    ctx.finalize_elementwise(self._ew_totals_buffer(), outs, out_dtype)
+                else:
+                    ctx.set_accumulated([1.0] * native.num_segments)
+                    ctx.finalize_range(outs, torch.float64)
+            elif not custom_divide and not host_divide:
                 if delta:
                     ctx.aggregate_delta(table, dt, self._delta_base(), outs, out_dtype)
                 else:
                     ctx.aggregate(table, dt or torch.float32, outs, out_dtype)
-                ctx.raise_on_nan(pending)
             else:
-                # a subclass divides: finalize with a unit divisor (exact), then call its hook
+                # fold the last wave, then divide by the host totals (exact float values of the
+                # reference's total objects) or by 1 for a subclass hook (exact: x / 1.0 == x)
                 if table is not None and dt is not None:
                     if delta:
                         ctx.accumulate_delta(table, dt, self._delta_base())
                     else:
                         ctx.accumulate(table, dt)
-                totals = ctx.total_weights()
-                ctx.set_accumulated([1.0] * native.num_segments)
-                ctx.finalize_range(outs, torch.float64)
-                ctx.raise_on_nan(pending)
+                if custom_divide:
+                    ctx.set_accumulated([1.0] * native.num_segments)
+                    ctx.finalize_range(outs, torch.float64)
+                else:
+                    ctx.set_accumulated([float(self.__host_totals[n]) for n in names])
+                    ctx.finalize_range(outs, out_dtype)
+            ctx.raise_on_nan(pending)
         except NaNAggregationError:
             ctx.reset()
             raise
         result: ModelParameter = {}
+        if custom_divide:
+            # a subclass's _apply_total_weight runs where the reference runs it — on host fp64
+            # tensors (torch's GPU division by a scalar multiplies by its reciprocal, which does
+            # not round like the reference's CPU division); one D2H copy of the weighted sums
+            host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+            host.copy_(flat)
         for j, i in enumerate(self.__keep):
             name = layout.names[i]
             value = outs[j].view(layout.shapes[i])
             if custom_divide:
-                value = self._apply_total_weight(name=name, parameter=value, total_weight=totals[j])
-                assert not value.isnan().any().cpu()
-                value = value.to(self.result_dtype)
+                total = self._total_for(name, j)
+                if isinstance(total, torch.Tensor):
+                    total = total.cpu()
+                value = host[offs[j] : offs[j] + native.numels[j]].view(layout.shapes[i])
+                value = self._apply_total_weight(name=name, parameter=value, total_weight=total)
+                assert not value.isnan().any()  # fed_avg_algorithm.py:97
+                value = value.to(device=self.device, dtype=self.result_dtype)
             result[name] = value
         ctx.reset()
         return result
+
+    def _total_for(self, name: str, seg: int) -> Any:
+        """The total object the reference hands _apply_total_weight (fed_avg_algorithm.py:95)."""
+        if not self.__ew:
+            return self.__host_totals[name]
+        ctx = self._context()
+        native = self.__native_layout
+        assert native is not None
+        o = ctx.segment_offset(seg)
+        tot = self._ew_totals_buffer()[o : o + native.numels[seg]].view(native.shapes[seg])
+        return tot.to(torch.float32) if self.__tot_fp32.get(name) else tot.clone()
 
     def aggregate_worker_data(self) -> ParameterMessage:
         parameter = self._aggregate_parameter()
@@ -433,7 +622,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         super().clear_worker_data()
         self.__table, self.__table_dtype = None, None
         self.__row = {}
-        self.__has_data = False
+        self._reset_round()
         if self.__ctx is not None:
             self.__ctx.reset()
 

@@ -1042,6 +1042,87 @@ __global__ __launch_bounds__(kThreads) void bw_read_kernel(const f32x4* __restri
 }
 
 // ---------------------------------------------------------------------------------------
+// Per-element weights: a _get_weight override that returns a tensor of the parameter's shape
+// (fed_avg_algorithm.py:51-62: `tmp = x.to(f64) * weight`, `acc += tmp`, `total += weight`, and
+// :94-96 `acc / total`, both elementwise). The total is a per-element buffer too; the reference
+// keeps it in the dtype of the first weight (torch's in-place add), so segments whose first weight
+// is fp32 round it to fp32 after every add (an fp32 sum of two fp32 values, computed in fp64 and
+// rounded once, is the correctly rounded fp32 sum). A NULL weight pointer takes a scalar weight
+// (names whose override returns a number). One workgroup per tile, clients in arrival order.
+// ---------------------------------------------------------------------------------------
+struct EwArgs {
+  const void* const* x;   // [T][K] compacted client pointers
+  const void* const* w;   // [T][K] weight pointers (NULL = scalar)
+  const double* ws;       // [T][K] scalar weights
+  const int32_t* wdt;     // [T][K] weight dtype (FEDAVG_F32 / FEDAVG_F64)
+  const int32_t* kseg;    // [T] clients of the segment in this call
+  const int32_t* flags;   // [T] bit 0: the accumulator holds data, bit 1: totals are fp32
+  int32_t stride;         // row stride of the [T][K] tables
+  double* acc;
+  double* tot;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void ew_fold_kernel(const TileDesc* __restrict__ tiles,
+                                                           const SegDesc* __restrict__ segs, EwArgs a) {
+  const TileDesc td = load_tile(tiles, blockIdx.x);
+  const int t = td.seg;
+  const int K = a.kseg[t];
+  const int f = a.flags[t];
+  const int64_t base = segs[t].acc_off + td.start;
+  for (int i = threadIdx.x; i < td.count; i += kThreads) {
+    bool have = (f & 1) != 0;
+    double s = have ? a.acc[base + i] : 0.0;
+    double tw = have ? a.tot[base + i] : 0.0;
+    for (int k = 0; k < K; ++k) {
+      const int64_t idx = static_cast<int64_t>(t) * a.stride + k;
+      const double x = load_g<T>(to_global<T>(a.x[idx]) + td.start, i);
+      const void* wp = a.w[idx];
+      double w = a.ws[idx];
+      if (wp != nullptr)
+        w = (a.wdt[idx] == FEDAVG_F32) ? static_cast<double>(static_cast<const float*>(wp)[td.start + i])
+                                       : static_cast<const double*>(wp)[td.start + i];
+      const double p = x * w;  // rounded, then added (no contraction: -ffp-contract=off)
+      if (have) {
+        s = s + p;
+        tw = tw + w;
+      } else {
+        s = p;
+        tw = w;
+        have = true;
+      }
+      if (f & 2) tw = static_cast<double>(static_cast<float>(tw));
+    }
+    a.acc[base + i] = s;
+    a.tot[base + i] = tw;
+  }
+}
+
+template <typename O>
+__global__ __launch_bounds__(kThreads) void ew_finalize_kernel(const TileDesc* __restrict__ tiles,
+                                                               const SegDesc* __restrict__ segs,
+                                                               const double* __restrict__ acc,
+                                                               const double* __restrict__ tot, void* const* outs,
+                                                               uint32_t* flag) {
+  const TileDesc td = load_tile(tiles, blockIdx.x);
+  const int64_t base = segs[td.seg].acc_off + td.start;
+  O* out = static_cast<O*>(reinterpret_cast<void*>(to_const<uint64_t>(outs)[td.seg])) + td.start;
+  bool bad_acc = false, bad_res = false;
+  for (int i = threadIdx.x; i < td.count; i += kThreads) {
+    const double v = acc[base + i];
+    const double r = v / tot[base + i];
+    bad_acc |= (v != v);
+    bad_res |= (r != r);
+    out[i] = static_cast<O>(r);
+  }
+  const uint64_t ba = __ballot(bad_acc), br = __ballot(bad_res);
+  if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+    if (ba) raise_flag(flag, 0);
+    if (br) raise_flag(flag, 1);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Scatter exchange of the multi-GPU round (sharded_comm.cpp): after the fp64
 // partials are reduce-scattered, rank r holds the global sums of an element window [lo, hi) of
 // the accumulator (any alignment, may span segments and their padding). It divides its window by
@@ -1162,6 +1243,12 @@ struct fedavg_ctx {
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
   std::vector<hipEvent_t> event_pool;
+  // auxiliary per-call tables (per-element weights, NaN scans): one pinned + device buffer pair
+  char* aux_host = nullptr;
+  char* aux_dev = nullptr;
+  size_t aux_cap = 0;
+  hipEvent_t aux_done = nullptr;  // the last upload out of aux_host finished
+  bool aux_used = false;
 };
 
 namespace {
@@ -1375,6 +1462,31 @@ int32_t stage_tables(fedavg_ctx* c, hipStream_t s, const void* const* client_ptr
     d = sl.dev;
   }
   L.point(d, st.tab);
+  return FEDAVG_OK;
+}
+
+// Upload a small per-call table blob through the context's auxiliary pinned buffer (the device
+// copy is ordered before the kernels that read it on the same stream).
+int32_t aux_upload(fedavg_ctx* c, hipStream_t s, const std::vector<char>& blob, char** dev) {
+  if (c->aux_used) FEDAVG_HIP_TRY(hipEventSynchronize(c->aux_done));
+  if (c->aux_cap < blob.size()) {
+    FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // a kernel may still read the old device table
+    if (c->aux_host) FEDAVG_HIP_TRY(hipHostFree(c->aux_host));
+    if (c->aux_dev) FEDAVG_HIP_TRY(hipFree(c->aux_dev));
+    c->aux_host = nullptr;
+    c->aux_dev = nullptr;
+    c->aux_cap = 0;
+    const size_t cap = std::max<size_t>(blob.size() * 2, 64 * 1024);
+    FEDAVG_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->aux_host), cap, hipHostMallocDefault));
+    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->aux_dev), cap));
+    c->aux_cap = cap;
+    if (!c->aux_done) FEDAVG_HIP_TRY(hipEventCreateWithFlags(&c->aux_done, hipEventDisableTiming));
+  }
+  std::memcpy(c->aux_host, blob.data(), blob.size());
+  FEDAVG_HIP_TRY(hipMemcpyAsync(c->aux_dev, c->aux_host, blob.size(), hipMemcpyHostToDevice, s));
+  FEDAVG_HIP_TRY(hipEventRecord(c->aux_done, s));
+  c->aux_used = true;
+  *dev = c->aux_dev;
   return FEDAVG_OK;
 }
 
@@ -1724,6 +1836,9 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->owns_acc && c->acc) (void)hipFree(c->acc);
+  if (c->aux_host) (void)hipHostFree(c->aux_host);
+  if (c->aux_dev) (void)hipFree(c->aux_dev);
+  if (c->aux_done) (void)hipEventDestroy(c->aux_done);
   delete c;
   return FEDAVG_OK;
 }
@@ -2175,6 +2290,113 @@ int32_t fedavg_plan_create_finalize(fedavg_ctx* c, const double* total_weights, 
     return r;
   }
   *out = p;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_set_segment_state(fedavg_ctx* c, const double* total_weights, const int32_t* valid) {
+  FEDAVG_RET(check_ctx(c));
+  if (!valid) return fail(FEDAVG_ERR_INVALID, "null valid flags");
+  for (int t = 0; t < c->T; ++t) {
+    c->valid[t] = valid[t] ? 1 : 0;
+    c->wsum[t] = (total_weights && valid[t]) ? total_weights[t] : -0.0;
+  }
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_accumulate_elementwise(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
+                                      const void* const* weight_ptrs, const int32_t* weight_dtypes,
+                                      const double* scalar_weights, const int32_t* total_fp32, int32_t K,
+                                      void* totals, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  if (K < 0) return fail(FEDAVG_ERR_INVALID, "num_clients < 0");
+  if (K == 0) return FEDAVG_OK;
+  if (!client_ptrs || !weight_ptrs || !weight_dtypes || !scalar_weights || !total_fp32 || !totals)
+    return fail(FEDAVG_ERR_INVALID, "null argument");
+  if (in_dtype != FEDAVG_F32 && in_dtype != FEDAVG_F16 && in_dtype != FEDAVG_BF16 && in_dtype != FEDAVG_F64)
+    return fail(FEDAVG_ERR_INVALID, "per-element weights take dense fp32 / fp16 / bf16 / fp64 inputs");
+  const int T = c->T;
+  for (int64_t i = 0; i < static_cast<int64_t>(K) * T; ++i)
+    if (weight_ptrs[i] && weight_dtypes[i] != FEDAVG_F32 && weight_dtypes[i] != FEDAVG_F64)
+      return fail(FEDAVG_ERR_INVALID, "per-element weights must be fp32 or fp64");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // segment-major compacted tables: x, w, ws, wdt ([T][K]), kseg, flags ([T])
+  const size_t TK = static_cast<size_t>(T) * K;
+  const size_t o_w = align_up(TK * 8, 16), o_ws = o_w + align_up(TK * 8, 16), o_wdt = o_ws + align_up(TK * 8, 16);
+  const size_t o_k = o_wdt + align_up(TK * 4, 16), o_f = o_k + align_up(static_cast<size_t>(T) * 4, 16);
+  std::vector<char> blob(o_f + align_up(static_cast<size_t>(T) * 4, 16), 0);
+  auto* hx = reinterpret_cast<const void**>(blob.data());
+  auto* hw = reinterpret_cast<const void**>(blob.data() + o_w);
+  auto* hs = reinterpret_cast<double*>(blob.data() + o_ws);
+  auto* hd = reinterpret_cast<int32_t*>(blob.data() + o_wdt);
+  auto* hk = reinterpret_cast<int32_t*>(blob.data() + o_k);
+  auto* hf = reinterpret_cast<int32_t*>(blob.data() + o_f);
+  for (int t = 0; t < T; ++t) {
+    int n = 0;
+    for (int k = 0; k < K; ++k) {
+      const size_t src = static_cast<size_t>(k) * T + t;
+      if (!client_ptrs[src]) continue;
+      const size_t dst = static_cast<size_t>(t) * K + n++;
+      hx[dst] = client_ptrs[src];
+      hw[dst] = weight_ptrs[src];
+      hs[dst] = scalar_weights[src];
+      hd[dst] = weight_dtypes[src];
+    }
+    hk[t] = n;
+    hf[t] = (c->valid[t] ? 1 : 0) | (total_fp32[t] ? 2 : 0);
+  }
+  char* d = nullptr;
+  FEDAVG_RET(aux_upload(c, s, blob, &d));
+  EwArgs a;
+  a.x = reinterpret_cast<const void* const*>(d);
+  a.w = reinterpret_cast<const void* const*>(d + o_w);
+  a.ws = reinterpret_cast<const double*>(d + o_ws);
+  a.wdt = reinterpret_cast<const int32_t*>(d + o_wdt);
+  a.kseg = reinterpret_cast<const int32_t*>(d + o_k);
+  a.flags = reinterpret_cast<const int32_t*>(d + o_f);
+  a.stride = K;
+  a.acc = c->acc;
+  a.tot = static_cast<double*>(totals);
+  const dim3 grid(static_cast<unsigned>(c->tiles1.size())), block(kThreads);
+  switch (in_dtype) {
+    case FEDAVG_F32: hipLaunchKernelGGL(ew_fold_kernel<float>, grid, block, 0, s, c->d_tiles1, c->d_segs, a); break;
+    case FEDAVG_F16: hipLaunchKernelGGL(ew_fold_kernel<__half>, grid, block, 0, s, c->d_tiles1, c->d_segs, a); break;
+    case FEDAVG_BF16: hipLaunchKernelGGL(ew_fold_kernel<bf16_t>, grid, block, 0, s, c->d_tiles1, c->d_segs, a); break;
+    default: hipLaunchKernelGGL(ew_fold_kernel<double>, grid, block, 0, s, c->d_tiles1, c->d_segs, a); break;
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  for (int t = 0; t < T; ++t)
+    if (hk[t] > 0) c->valid[t] = 1;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_finalize_elementwise(fedavg_ctx* c, const void* totals, void* const* out_ptrs, int32_t out_dtype,
+                                    void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (!totals || !out_ptrs) return fail(FEDAVG_ERR_INVALID, "null argument");
+  for (int t = 0; t < c->T; ++t) {
+    if (!c->valid[t])
+      return fail(FEDAVG_ERR_STATE, "segment " + std::to_string(t) + " has no accumulated data (fed_avg_algorithm.py:88)");
+    if (!out_ptrs[t]) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+  }
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::vector<char> blob(align_up(sizeof(void*) * c->T, 16));
+  std::memcpy(blob.data(), out_ptrs, sizeof(void*) * c->T);
+  char* d = nullptr;
+  FEDAVG_RET(aux_upload(c, s, blob, &d));
+  const dim3 grid(static_cast<unsigned>(c->tiles1.size())), block(kThreads);
+  const auto* tot = static_cast<const double*>(totals);
+  auto* outs = reinterpret_cast<void* const*>(d);
+  if (ok == OUT_F32)
+    hipLaunchKernelGGL(ew_finalize_kernel<float>, grid, block, 0, s, c->d_tiles1, c->d_segs, c->acc, tot, outs, c->d_flag);
+  else
+    hipLaunchKernelGGL(ew_finalize_kernel<double>, grid, block, 0, s, c->d_tiles1, c->d_segs, c->acc, tot, outs, c->d_flag);
+  FEDAVG_HIP_TRY(hipGetLastError());
+  std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
+  std::fill(c->valid.begin(), c->valid.end(), 0);
   return FEDAVG_OK;
 }
 

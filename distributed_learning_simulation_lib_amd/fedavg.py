@@ -136,20 +136,47 @@ class ClientTable:
         self._keep: list[torch.Tensor] = []
         self.num_clients = 0
         self._arrays: tuple[np.ndarray, np.ndarray] | None = None
+        # per-element weights (fedavg_accumulate_elementwise): pointer + dtype code per entry
+        self._wptrs: list[int] = []
+        self._wdts: list[int] = []
 
-    def add_client(self, tensors: Sequence[torch.Tensor | None], weights: Sequence[float]) -> None:
+    def add_client(self, tensors: Sequence[torch.Tensor | None], weights: Sequence[float],
+                   weight_tensors: Sequence[torch.Tensor | None] | None = None) -> None:
+        """One client row. ``weight_tensors`` (optional): per-element weight tensors (fp32 / fp64,
+        the segment's size) where a _get_weight override returned one; None = the scalar."""
         if len(tensors) != self.num_segments or len(weights) != self.num_segments:
             raise ValueError("client row does not match the layout")
-        for t, w in zip(tensors, weights):
+        if weight_tensors is None:
+            weight_tensors = [None] * self.num_segments
+        elif len(weight_tensors) != self.num_segments:
+            raise ValueError("weight row does not match the layout")
+        for t, w, wt in zip(tensors, weights, weight_tensors):
             if t is None:
                 self._ptrs.append(0)
                 self._weights.append(0.0)
+                self._wptrs.append(0)
+                self._wdts.append(_native.F64)
             else:
                 self._ptrs.append(t.data_ptr())
                 self._weights.append(float(w))
                 self._keep.append(t)
+                if wt is None:
+                    self._wptrs.append(0)
+                    self._wdts.append(_native.F64)
+                else:
+                    if wt.dtype not in (torch.float32, torch.float64) or not wt.is_contiguous() \
+                            or wt.numel() != t.numel() or wt.device != t.device:
+                        raise ValueError("per-element weights: contiguous fp32 / fp64 of the tensor's size and device")
+                    self._wptrs.append(wt.data_ptr())
+                    self._wdts.append(_native.F32 if wt.dtype == torch.float32 else _native.F64)
+                    self._keep.append(wt)
         self.num_clients += 1
         self._arrays = None
+
+    def elementwise_arrays(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Weight pointers and dtype codes, [num_clients][num_segments] (0 = scalar weight)."""
+        return (np.asarray(self._wptrs or [0], dtype=np.uint64), np.asarray(self._wdts or [0], dtype=np.int32),
+                np.asarray(self._weights or [0.0], dtype=np.float64))
 
     def arrays(self) -> tuple[np.ndarray, np.ndarray]:
         """The C-ABI arrays (built once per table and cached: a table can be reduced many times)."""
@@ -385,6 +412,37 @@ class FedAvgContext:
                 w.ctypes.data_as(_DBL), n, 1 if zero_init else 0, tile_begin, tile_end, self.stream,
             )
         )
+
+    def set_segment_state(self, total_weights: Sequence[float], valid: Sequence[int]) -> None:
+        """Per-segment accumulated state (a layout grown mid-round keeps its folded segments)."""
+        tw = (ctypes.c_double * self.layout.num_segments)(*[float(x) for x in total_weights])
+        vv = (ctypes.c_int32 * self.layout.num_segments)(*[1 if v else 0 for v in valid])
+        _native.check(self._lib.fedavg_set_segment_state(self._h, tw, vv))
+
+    def accumulate_elementwise(self, table: ClientTable, in_dtype: torch.dtype, totals: torch.Tensor,
+                               total_fp32: Sequence[bool]) -> None:
+        """Fold a wave with per-element weights (fed_avg_algorithm.py:51-62 with a tensor-valued
+        _get_weight): acc += x * w and totals += w elementwise; ``totals`` is an fp64 buffer in
+        accumulator coordinates, rounded to fp32 per segment where ``total_fp32``."""
+        self._check_table(table, in_dtype)
+        if table.num_clients == 0:
+            return
+        if totals.dtype != torch.float64 or totals.numel() < self.acc_numel or totals.device != self.device:
+            raise ValueError("totals: an fp64 buffer of the accumulator's size on the context device")
+        p, _ = table.arrays()
+        wp, wd, ws = table.elementwise_arrays()
+        flags = (ctypes.c_int32 * self.layout.num_segments)(*[1 if f else 0 for f in total_fp32])
+        _native.check(self._lib.fedavg_accumulate_elementwise(
+            self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), wp.ctypes.data_as(_PTR),
+            wd.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ws.ctypes.data_as(_DBL), flags, table.num_clients,
+            ctypes.c_void_p(totals.data_ptr()), self.stream))
+
+    def finalize_elementwise(self, totals: torch.Tensor, outs: Sequence[torch.Tensor] | OutputTable,
+                             out_dtype: torch.dtype) -> None:
+        """out = acc / totals elementwise (fed_avg_algorithm.py:94-97); resets the state."""
+        ot = self._out_table(outs, out_dtype)
+        _native.check(self._lib.fedavg_finalize_elementwise(self._h, ctypes.c_void_p(totals.data_ptr()), ot,
+                                                            out_code(out_dtype), self.stream))
 
     def set_accumulated(self, total_weights: Sequence[float]) -> None:
         tw = (ctypes.c_double * self.layout.num_segments)(*[float(x) for x in total_weights])

@@ -249,6 +249,32 @@ int32_t fedavg_plan_create_finalize(fedavg_ctx* ctx, const double* total_weights
                                     void* const* out_ptrs, int32_t out_dtype, fedavg_plan** out);
 int32_t fedavg_plan_run_range(fedavg_plan* plan, int32_t tile_begin, int32_t tile_end, void* stream);
 
+/*
+ * Move accumulated state between contexts (a layout that grows when a tensor name first appears
+ * in a later client, fed_avg_algorithm.py:55-62): per segment, valid[t] != 0 marks the
+ * accumulator as holding data with total weight total_weights[t] (NULL: -0.0); valid[t] == 0
+ * makes the next fold of that segment an assignment.
+ */
+int32_t fedavg_set_segment_state(fedavg_ctx* ctx, const double* total_weights, const int32_t* valid);
+
+/*
+ * Per-element weights (a _get_weight override returning a tensor of the parameter's shape,
+ * fed_avg_algorithm.py:51-62, divided elementwise at :94-96):
+ *   acc[e] = (acc_in ? acc[e] + round(x[e] * w[e]) : round(x[e] * w[e]))
+ *   tot[e] = (acc_in ? tot[e] + w[e] : w[e]), rounded to fp32 after every add when
+ *            total_fp32[t] (the reference keeps the total in the first weight's dtype)
+ * weight_ptrs[K][T]: device fp32 / fp64 (weight_dtypes[K][T]) tensors of the segment's size, or
+ * NULL = the scalar scalar_weights[k][t]; totals: fp64 device buffer in accumulator coordinates
+ * (fedavg_acc_numel elements), owned by the caller. fedavg_finalize_elementwise writes
+ * out = acc / tot (IEEE, fp32 / fp64), with the :93 / :97 NaN checks, and resets the state.
+ */
+int32_t fedavg_accumulate_elementwise(fedavg_ctx* ctx, const void* const* client_ptrs, int32_t in_dtype,
+                                      const void* const* weight_ptrs, const int32_t* weight_dtypes,
+                                      const double* scalar_weights, const int32_t* total_fp32, int32_t num_clients,
+                                      void* totals, void* stream);
+int32_t fedavg_finalize_elementwise(fedavg_ctx* ctx, const void* totals, void* const* out_ptrs, int32_t out_dtype,
+                                    void* stream);
+
 /* Pieces of the scatter exchange (fedavg_sharded_round_scatter; also usable from a host-driven
  * exchange, sharded.py). `finalize` is a finalize plan (its totals, outputs and out dtype).
  *  fedavg_plan_finalize_window: res[p] = src[p - lo] / W[seg(p)] for accumulator positions p in

@@ -36,6 +36,8 @@ import torch
 
 REF = Path("/root/reference")
 OUT_DIR = Path(__file__).resolve().parent
+sys.path.insert(0, str(OUT_DIR.parent.parent))  # the repo root: tests.golden_hooks
+from tests.golden_hooks import make_hooked_class  # noqa: E402  (the cases' overridden hooks)
 
 
 def _load_reference():
@@ -107,7 +109,8 @@ def build_cases():
             arrivals.append((k, _model(shapes, dtype, seed + k), weights[k], {}))
         cases.append(dict(name=name, shapes=shapes, dtype=dtype, arrivals=arrivals,
                           accumulate=kw.get("accumulate", True), aggregate_loss=False,
-                          per_tensor_weight=None, expect_error=None))
+                          per_tensor_weight=None, expect_error=None, weight_mode=None,
+                          total_weight_hook=None))
         return cases[-1]
 
     add("n1_f32", {"a": (7,), "b": (3, 5), "c": (33, 17)}, torch.float32, 1, [250], 1)
@@ -182,6 +185,38 @@ def build_cases():
     c["kinds"] = ["delta", "delta", "full", "delta", "delta"]
     c["arrivals"][2] = (2, {k: v.to(torch.float32) for k, v in c["arrivals"][2][1].items()}, 33, {})
 
+    # a key that first appears in a later client (fed_avg_algorithm.py:55-62 grow the per-name
+    # dicts): output keys in first-seen order, per-name totals over the clients that sent it
+    c = add("late_key", {"a": (300,), "b": (4099,), "c": (5, 3)}, torch.float32, 4, [7, 2, 9, 4], 58)
+    del c["arrivals"][0][1]["b"], c["arrivals"][0][1]["c"]
+    del c["arrivals"][1][1]["c"]
+    del c["arrivals"][2][1]["a"]
+
+    # _apply_total_weight overridden by a subclass (fed_avg_algorithm.py:71-74, used at :94-96);
+    # the hook sees the per-name total and the fp64 weighted sum
+    c = add("total_weight_hook", {"o0": (2050,), "o1": (6, 7)}, torch.float32, 5, _ds_weights(5, 59), 59)
+    c["total_weight_hook"] = "scaled"
+
+    # tensor-valued _get_weight (fed_avg_algorithm.py:51-54,66-69: `tmp = x.to(f64) * weight`,
+    # `total += weight`): a fresh 0-dim tensor per (client, tensor) — the totals then accumulate in
+    # the tensor's dtype — or a per-element weight tensor of the parameter's shape
+    fw = [float(x) for x in np.random.default_rng(70).uniform(0.1, 10.0, 6)]
+    c = add("weight_tensor_f32", {"s0": (1500,), "s1": (9,)}, torch.float32, 6, fw, 70)
+    c["weight_mode"] = "scalar_tensor_float32"
+    c = add("weight_tensor_f64", {"s0": (1500,), "s1": (9,)}, torch.float32, 6, fw, 71)
+    c["weight_mode"] = "scalar_tensor_float64"
+    for wdt, seed in (("float64", 72), ("float32", 73)):
+        # (aggregation_weight is the arrival's row in elem_weights, as in per_tensor_weight)
+        c = add(f"weight_elementwise_f{wdt[5:]}", {"e0": (2500,), "e1": (3, 11), "e2": ()}, torch.float32, 5,
+                [0, 1, 2, 3, 4], seed)
+        c["weight_mode"] = f"elementwise_{wdt}"
+        g = torch.Generator().manual_seed(seed * 7)
+        c["elem_weights"] = [
+            {n: (torch.rand(sh, generator=g, dtype=torch.float64) * 4 + 0.25).to(getattr(torch, wdt))
+             for n, sh in c["shapes"].items()}
+            for _ in range(5)
+        ]
+
     # ---- errors ----
     c = add("err_nan_input", {"e": (100,)}, torch.float32, 3, [1, 2, 3], 60)
     c["arrivals"][1][1]["e"][17] = float("nan")
@@ -204,19 +239,11 @@ def build_cases():
 
 def run_reference(case, message, fed):
     """Drive the reference's FedAVGAlgorithm exactly like AggregationServer does."""
-    FedAVG = fed.FedAVGAlgorithm
-    ptw = case["per_tensor_weight"]
-    if ptw is not None:
-        class PerTensor(FedAVG):  # overrides the reference's hook
-            def _get_weight(self, worker_data, name, parameter):
-                return ptw[name][int(worker_data.aggregation_weight)]
-        algo = PerTensor()
-    else:
-        algo = FedAVG()
+    algo = make_hooked_class(fed.FedAVGAlgorithm, case)()
     algo.accumulate = case["accumulate"]
     algo.aggregate_loss = case["aggregate_loss"]
     kinds = case.get("kinds") or ["full"] * len(case["arrivals"])
-    for (wid, params, weight, other), kind in zip(case["arrivals"], kinds):
+    for j, ((wid, params, weight, other), kind) in enumerate(zip(case["arrivals"], kinds)):
         if params is None:
             algo.process_worker_data(worker_id=wid, worker_data=None)
             continue
@@ -232,7 +259,7 @@ def run_reference(case, message, fed):
             if "old" in case:
                 msg.complete(case["old"])
         algo.process_worker_data(worker_id=wid, worker_data=msg)
-    return algo.aggregate_worker_data()
+    return algo.aggregate_worker_data(), getattr(algo, "seen_totals", None)
 
 
 def _np(t: torch.Tensor) -> np.ndarray:
@@ -264,6 +291,8 @@ def main() -> int:
             "per_tensor_weight": case["per_tensor_weight"],
             "arrivals": [],
             "kinds": case.get("kinds"),
+            "weight_mode": case.get("weight_mode"),
+            "total_weight_hook": case.get("total_weight_hook"),
         }
         if "old" in case:
             entry["old_keys"] = list(case["old"].keys())
@@ -275,9 +304,12 @@ def main() -> int:
             if params is not None:
                 for k, v in params.items():
                     arrays[f"{name}/in/{j}/{k}"] = _np(v)
+            if case.get("elem_weights") is not None:
+                for k, v in case["elem_weights"][j].items():
+                    arrays[f"{name}/w/{j}/{k}"] = v.numpy()
             entry["arrivals"].append(a)
         try:
-            res = run_reference(case, message, fed)
+            res, hook_totals = run_reference(case, message, fed)
         except (AssertionError, RuntimeError) as e:
             entry["error"] = type(e).__name__
             if case["expect_error"] is not None:
@@ -292,6 +324,7 @@ def main() -> int:
             entry["result_other_data"] = res.other_data
             entry["end_training"] = res.end_training
             entry["in_round"] = res.in_round
+            entry["hook_totals"] = hook_totals
         manifest["cases"].append(entry)
         print(f"{name}: {'error ' + entry['error'] if entry['error'] else 'ok'}")
     np.savez_compressed(OUT_DIR / "fedavg_golden.npz", **arrays)

@@ -19,6 +19,7 @@ class Arrival:
     weight: Any
     other_data: dict
     arrays: dict[str, np.ndarray] | None  # raw (bf16 as uint16 bits)
+    elem_weights: dict[str, np.ndarray] | None = None  # per-element _get_weight values (weight_mode)
 
 
 @dataclass
@@ -36,6 +37,10 @@ class GoldenCase:
     meta: dict
     kinds: list[str] | None = None  # per arrival "full" / "delta" (delta: against `old`)
     old: dict[str, np.ndarray] | None = None
+    # overridden hooks (gen_golden.make_hooked_class): None, "scalar_tensor_float32/64",
+    # "elementwise_float32/64"; total_weight_hook: None or "scaled" ((x * 3) / (W + 1))
+    weight_mode: str | None = None
+    total_weight_hook: str | None = None
 
     def torch_params(self, arrival: Arrival, device: torch.device | str = "cpu") -> dict[str, torch.Tensor]:
         assert arrival.arrays is not None
@@ -60,7 +65,10 @@ def load_golden() -> dict[str, GoldenCase]:
             arrays = None
             if a["keys"] is not None:
                 arrays = {k: data[f"{name}/in/{j}/{k}"] for k in a["keys"]}
-            arrivals.append(Arrival(a["worker_id"], a["weight"], dict(a["other_data"]), arrays))
+            ew = None
+            if (c.get("weight_mode") or "").startswith("elementwise") and a["keys"] is not None:
+                ew = {k: data[f"{name}/w/{j}/{k}"] for k in c["names"]}
+            arrivals.append(Arrival(a["worker_id"], a["weight"], dict(a["other_data"]), arrays, ew))
         expected = None
         if c["error"] is None:
             expected = {k: data[f"{name}/out/{k}"] for k in c["out_keys"]}
@@ -78,6 +86,8 @@ def load_golden() -> dict[str, GoldenCase]:
             meta=c,
             kinds=c.get("kinds"),
             old={k: data[f"{name}/old/{k}"] for k in c["old_keys"]} if c.get("old_keys") else None,
+            weight_mode=c.get("weight_mode"),
+            total_weight_hook=c.get("total_weight_hook"),
         )
     return cases
 

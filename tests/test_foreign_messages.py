@@ -29,7 +29,7 @@ class RecordingFedAvg(FedAVGAlgorithm):
         super().__init__(device="cpu", **kw)
         self.staged: list[tuple[dict, bool]] = []
 
-    def _stage_client(self, delta: bool = False) -> None:
+    def _stage_client(self, delta: bool = False, worker_id=None) -> None:
         row = self._FedAVGAlgorithm__row  # the staged (tensor, weight) row of this arrival
         self._FedAVGAlgorithm__row = {}
         self.staged.append((dict(row), delta))

@@ -27,6 +27,7 @@ from distributed_learning_simulation_lib_amd import message as _pkg_message
 from distributed_learning_simulation_lib_amd.algorithm import AggregationAlgorithm
 from distributed_learning_simulation_lib_amd.fedavg import ClientTable, FedAvgContext, ModelLayout, bw_probe
 from oracle.fedavg_oracle import as_f64, fedavg_flat
+from tests.golden_hooks import make_hooked_class
 from tests.golden_io import bits_equal, load_golden
 
 pytestmark = pytest.mark.gpu
@@ -34,19 +35,24 @@ CASES = load_golden()
 TORCH_DT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16, "float64": torch.float64}
 
 
-def run_hip(case, device, wave_size, from_host=False, split_policy=1, wire=None, delta_checks=False):
+def hook_spec(case):
+    """The golden case's hooks (tests/golden_hooks.py) with its per-element weights as tensors."""
+    elem = None
+    if case.weight_mode is not None and case.weight_mode.startswith("elementwise"):
+        elem = [{k: torch.from_numpy(v.copy()) for k, v in a.elem_weights.items()} if a.elem_weights else None
+                for a in case.arrivals]
+    return {"per_tensor_weight": case.per_tensor_weight, "weight_mode": case.weight_mode,
+            "total_weight_hook": case.total_weight_hook, "elem_weights": elem}
+
+
+def run_hip(case, device, wave_size, from_host=False, split_policy=1, wire=None, delta_checks=False, algo_out=None,
+            **algo_kw):
     """Drive the plugin like AggregationServer does. ``wire``: the message module (default this
     package's; tests.foreign_messages = another class hierarchy with the same schema, as the
     reference server passes). ``delta_checks``: deltas carry new_parameter (not fusable)."""
     wire = wire or _pkg_message
-    ptw = case.per_tensor_weight
-    if ptw is not None:
-        class PerTensor(FedAVGAlgorithm):
-            def _get_weight(self, worker_data, name, parameter):
-                return ptw[name][int(worker_data.aggregation_weight)]
-        algo = PerTensor(device=device, wave_size=wave_size, split_policy=split_policy)
-    else:
-        algo = FedAVGAlgorithm(device=device, wave_size=wave_size, split_policy=split_policy)
+    algo = make_hooked_class(FedAVGAlgorithm, hook_spec(case))(device=device, wave_size=wave_size,
+                                                               split_policy=split_policy, **algo_kw)
     algo.accumulate = case.accumulate
     algo.aggregate_loss = case.aggregate_loss
     kinds = case.kinds or ["full"] * len(case.arrivals)
@@ -69,6 +75,8 @@ def run_hip(case, device, wave_size, from_host=False, split_policy=1, wire=None,
             if old is not None:
                 msg.complete(old)
         algo.process_worker_data(a.worker_id, msg)
+    if algo_out is not None:
+        algo_out.append(algo)
     try:
         return algo.aggregate_worker_data()
     finally:
@@ -92,6 +100,41 @@ def test_plugin_matches_reference_bitwise(name, wave_size, hip_device):
         assert bits_equal(got.cpu().numpy(), want), f"{name}/{k}"
     assert res.other_data == case.meta["result_other_data"]
     assert res.in_round == case.meta["in_round"] and res.end_training == case.meta["end_training"]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_plugin_result_on_the_host_bitwise(name, hip_device):
+    """result_device="cpu" (the reference's server caches host fp64 tensors): one pinned D2H copy
+    of the flat result, same bits, host tensors."""
+    case = CASES[name]
+    if case.error is not None or not case.accumulate:
+        return
+    res = run_hip(case, hip_device, 64, result_device="cpu")
+    for k, want in case.expected.items():
+        got = res.parameter[k]
+        assert got.device.type == "cpu" and got.dtype == torch.float64
+        assert bits_equal(got.numpy(), want), f"{name}/{k}"
+
+
+def test_total_weight_hook_receives_the_reference_totals(hip_device):
+    case = CASES["total_weight_hook"]
+    algos = []
+    run_hip(case, hip_device, 2, algo_out=algos)
+    assert algos[0].seen_totals == case.meta["hook_totals"]
+
+
+def test_eager_nan_check_fails_the_arrival(hip_device):
+    """eager_nan_check: fed_avg_algorithm.py:35 fires while the offending update arrives."""
+    case = CASES["err_nan_input"]
+    algo = FedAVGAlgorithm(device=hip_device, eager_nan_check=True)
+    a0, a1 = case.arrivals[0], case.arrivals[1]
+    algo.process_worker_data(a0.worker_id, ParameterMessage(parameter=case.torch_params(a0, hip_device),
+                                                            aggregation_weight=a0.weight))
+    with pytest.raises(NaNAggregationError) as ei:
+        algo.process_worker_data(a1.worker_id, ParameterMessage(parameter=case.torch_params(a1, "cpu"),
+                                                                aggregation_weight=a1.weight))
+    assert ei.value.stage == "input" and ei.value.bad_clients == [a1.worker_id]
+    algo.exit()
 
 
 @pytest.mark.parametrize("name", sorted(CASES))

@@ -534,8 +534,9 @@ def main() -> int:
     ap.add_argument("--clients-per-gpu", type=int, default=64,
                     help="weak scaling (--weak) and the personalized / qsgd workloads: clients per GPU")
     ap.add_argument("--total-clients", type=int, default=0,
-                    help="clients of the whole job, sharded over the ranks (0 = auto: 64 on one GPU = "
-                         "BASELINE config 2; 256 on N > 1 GPUs = BASELINE config 3, strong scaling)")
+                    help="clients of the whole job, sharded over the ranks (0 = auto: --clients-per-gpu "
+                         "(64) on one GPU = BASELINE config 2; 256 on N > 1 GPUs = BASELINE config 3, "
+                         "strong scaling)")
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling instead: --clients-per-gpu clients on every rank")
     ap.add_argument("--wave", type=int, default=0, help="clients per launch (streaming waves); 0 = all")
@@ -596,7 +597,8 @@ def main() -> int:
     elif args.total_clients > 0:
         n_total = args.total_clients
     else:
-        n_total = 256 if world > 1 else 64  # BASELINE.json configs[2] / configs[1]
+        # BASELINE.json configs[2] (256 clients over the GPUs) / one GPU: configs[1] (64 clients)
+        n_total = 256 if world > 1 else args.clients_per_gpu
     # contiguous client shards: rank r folds clients [lo, hi) (N/G each; the dispatcher's split)
     lo, hi = rank * n_total // world, (rank + 1) * n_total // world
     n_local = hi - lo

@@ -110,6 +110,17 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_NT_STORE
 #define FEDAVG_NT_STORE 1
 #endif
+// Software-pipelined client loads (the next stage's loads issue before the current stage folds),
+// one bit per input size: 1 = 2-byte, 2 = 4-byte, 4 = 8-byte. Interleaved A/B on MI355X
+// (scripts/tune_kernel.py, 64-byte stages = 4 fp16 / bf16 clients): 64 x ResNet-18 fp16
+// 0.2672 -> 0.2618 ms, bf16 0.2755 -> 0.2628 ms, 128 x GPT-2 fp16 5.443 -> 5.422 ms; 128 / 256-B
+// stages no better; fp32 with 128 / 256-B stages 13 % / 10 % slower (kept grouped).
+#ifndef FEDAVG_PIPE
+#define FEDAVG_PIPE 1
+#endif
+#ifndef FEDAVG_PIPE_BYTES  // bytes of client loads per lane per pipeline stage
+#define FEDAVG_PIPE_BYTES 64
+#endif
 constexpr int kAE = FEDAVG_AE;    // elements owned by one lane (fp64 accumulators per lane)
 constexpr int kTile1 = FEDAVG_TILE1;          // 4096 elements, SPLIT = 1 (any dtype)
 #ifndef FEDAVG_TILE_WIDE  // whole-layout exact-order launches of 2- and 4-byte inputs (0 = off)
@@ -498,7 +509,68 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   // a group are issued before any is consumed. A short last group (TAIL) re-loads its last
   // client for the missing slots (L2 hits) and masks them out of the fold with selects —
   // never with branches, which made hipcc serialise the loads.
-  if constexpr (FAST) {
+  constexpr bool PIPE = FAST && ((FEDAVG_PIPE >> (sizeof(T) == 2 ? 0 : sizeof(T) == 4 ? 1 : 2)) & 1);
+  if constexpr (PIPE) {
+    // Software-pipelined form: the next stage's client loads are issued before the current
+    // stage folds, so a lane keeps HBM requests in flight through its own fold work (the
+    // grouped form below leaves the lane's memory pipe idle while it folds a group). Stages
+    // of PG clients alternate between two register buffers; the stage after the last one
+    // re-loads the last client (an L2 hit, never folded) so every stage issues the same loads
+    // and the code stays branch-free.
+    constexpr int PB = FEDAVG_PIPE_BYTES;
+    constexpr int PG = (PB / (VPL * 16)) < 1 ? 1 : (PB / (VPL * 16));
+    V bufA[PG][VPL], bufB[PG][VPL];
+    double wA[PG], wB[PG];
+    auto load_stage = [&](V (&buf)[PG][VPL], double (&wk)[PG], int k) {
+#pragma unroll
+      for (int c = 0; c < PG; ++c) {
+        const int kc = min(k + c, ke - 1);
+        wk[c] = wp[kc];
+        LL::load_raw(client(kc), li, buf[c]);
+      }
+    };
+    auto fold_stage = [&](auto tail_tag, V (&buf)[PG][VPL], const double (&wk)[PG], int n) {
+      constexpr bool TAIL = decltype(tail_tag)::value;
+#pragma unroll
+      for (int c = 0; c < PG; ++c) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          double x[N];
+          expand<T>(buf[c][v], x);
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            double& r = acc[v * N + j];
+            const double nv = fold<FOLD>(r, x[j], wk[c], base[v * N + j]);
+            if constexpr (TAIL) {
+              r = (c < n) ? nv : r;
+            } else {
+              r = nv;
+            }
+          }
+        }
+      }
+    };
+    if (kb < ke) {
+      int k = kb;
+      load_stage(bufA, wA, k);
+      // full stages two at a time (A folds while B loads, then B folds while A loads)
+      while (k + 2 * PG <= ke) {
+        load_stage(bufB, wB, k + PG);
+        fold_stage(std::false_type{}, bufA, wA, PG);
+        load_stage(bufA, wA, k + 2 * PG);
+        fold_stage(std::false_type{}, bufB, wB, PG);
+        k += 2 * PG;
+      }
+      // 0 < ke - k < 2 * PG clients left; bufA holds stage k
+      if (k + PG < ke) {
+        load_stage(bufB, wB, k + PG);
+        fold_stage(std::false_type{}, bufA, wA, PG);
+        fold_stage(std::true_type{}, bufB, wB, ke - k - PG);
+      } else if (k < ke) {
+        fold_stage(std::true_type{}, bufA, wA, ke - k);
+      }
+    }
+  } else if constexpr (FAST) {
     auto group = [&](auto tail_tag, int k, int n) {
       constexpr bool TAIL = decltype(tail_tag)::value;
       V buf[CU_LOADS][VPL];

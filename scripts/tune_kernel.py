@@ -13,8 +13,11 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "d64w16": {"FEDAVG_F64_WIDE": 1, "FEDAVG_AE_F64_WIDE": 16},
-    "d64w16_cu1k": {"FEDAVG_F64_WIDE": 1, "FEDAVG_AE_F64_WIDE": 16, "FEDAVG_CU_BYTES_F64": 1024},
+    "pipe_h64": {"FEDAVG_PIPE": 1, "FEDAVG_PIPE_BYTES": 64},
+    "pipe_h128": {"FEDAVG_PIPE": 1, "FEDAVG_PIPE_BYTES": 128},
+    "pipe_h256": {"FEDAVG_PIPE": 1, "FEDAVG_PIPE_BYTES": 256},
+    "pipe_f128": {"FEDAVG_PIPE": 2, "FEDAVG_PIPE_BYTES": 128},
+    "pipe_f256": {"FEDAVG_PIPE": 2, "FEDAVG_PIPE_BYTES": 256},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

@@ -5,6 +5,8 @@
 //   2. per arriving client: fedavg_accumulate (streaming, fed_avg_algorithm.py:43-64)
 //   3. fedavg_aggregate: ÷ total weight into fp32 / fp64 outputs (:76-99) + fedavg_check
 //   4. the multi-GPU exchange on a one-rank RCCL world: fedavg_comm_* + fedavg_sharded_round
+//      (reduce to the root) and fedavg_sharded_round_scatter (reduce-scatter + window finalize +
+//      gather)
 //
 // Self-check: the streamed result and the sharded result are compared bit-for-bit with a plain
 // fp64 host fold in arrival order (acc = -0.0; acc += double(x) * w; out = acc / W) — the
@@ -146,6 +148,13 @@ int main() {
     CHECK_ST(fedavg_sharded_round(comm, ctx, partial, finalize, 4, 0, stream));
     CHECK_ST(fedavg_check(ctx, stream, nullptr));
     if (compare(round == 0 ? "sharded round 1" : "sharded round 2")) return 1;
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int t = 0; t < T; ++t) CHECK_HIP(hipMemsetAsync(out[t], 0xFF, numel[t] * sizeof(double), stream));
+    CHECK_ST(fedavg_reset(ctx, stream));
+    CHECK_ST(fedavg_sharded_round_scatter(comm, ctx, partial, finalize, 3, 0, stream));
+    CHECK_ST(fedavg_check(ctx, stream, nullptr));
+    if (compare(round == 0 ? "scatter round 1" : "scatter round 2")) return 1;
   }
 
   CHECK_ST(fedavg_comm_destroy(comm));

@@ -1311,6 +1311,9 @@ struct fedavg_ctx {
   int split_policy = 1;  // 1 exact client order (default), 0 auto, 2 always split
   bool allow_fma = true;  // fused fold when every product is provably exact
   int persistent_blocks = 0;  // grid cap of the exact-order kernel (0 = one block per tile)
+  // whole-layout launches use the wide tile table only when they fold at least this many clients
+  // per segment (short waves keep the 4096-element tiles: two workgroups per CU instead of one)
+  int wide_min_clients = 0;
   // profiling
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -1668,6 +1671,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   }
   // whole-layout exact-order launch of a 2- / 4-byte input: the wide table (same elements)
   const bool wide = split == 1 && c->d_tilesw != nullptr && c->persistent_blocks == 0 && tb_split1 == 0 &&
+                    st.Kmax >= c->wide_min_clients &&
                     te_split1 == static_cast<int32_t>(c->tiles1.size()) &&
                     (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F16 || in_dtype == FEDAVG_BF16 ||
                      (FEDAVG_F64_WIDE && in_dtype == FEDAVG_F64));
@@ -1820,6 +1824,7 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   }
   c->acc_numel = off;
   c->wsum.assign(num_segments, -0.0);  // additive identity: the first weight is taken as is
+  if (const char* e = std::getenv("FEDAVG_WIDE_MIN_CLIENTS")) c->wide_min_clients = std::atoi(e);
   c->valid.assign(num_segments, 0);
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);

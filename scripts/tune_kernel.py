@@ -13,11 +13,8 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "pipe_h64": {"FEDAVG_PIPE": 1, "FEDAVG_PIPE_BYTES": 64},
-    "pipe_h128": {"FEDAVG_PIPE": 1, "FEDAVG_PIPE_BYTES": 128},
-    "pipe_h256": {"FEDAVG_PIPE": 1, "FEDAVG_PIPE_BYTES": 256},
-    "pipe_f128": {"FEDAVG_PIPE": 2, "FEDAVG_PIPE_BYTES": 128},
-    "pipe_f256": {"FEDAVG_PIPE": 2, "FEDAVG_PIPE_BYTES": 256},
+    "accpl_h": {"FEDAVG_ACC_PLAIN_STORE_HALF": 1},
+    "ntst0": {"FEDAVG_NT_STORE": 0},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 
@@ -48,9 +45,25 @@ def run_all(rounds=7, iters=10):
     dt = getattr(torch, sys.argv[4]) if len(sys.argv) > 4 else torch.float32
     buckets, views = make_clients(layout, 0, K, dev, dt)
     w = dataset_size_weights(K)
-    table = ClientTable(layout.num_segments)
-    for row, wk in zip(views, w):
-        table.add_client(row, [wk] * layout.num_segments)
+    wave = int(sys.argv[5]) if len(sys.argv) > 5 and int(sys.argv[5]) > 0 else K  # clients per launch (waves)
+    tables = []
+    for w0 in range(0, K, wave):
+        t = ClientTable(layout.num_segments)
+        for row, wk in zip(views[w0 : w0 + wave], w[w0 : w0 + wave]):
+            t.add_client(row, [wk] * layout.num_segments)
+        tables.append(t)
+    table = tables[-1]
+
+    class Waves:
+        """aggregate() of the whole job: earlier waves accumulated, the last one fused."""
+
+        def __init__(self, ctx):
+            self.ctx = ctx
+
+        def aggregate(self, _t, dt_, outs_, odt):
+            for t in tables[:-1]:
+                self.ctx.accumulate(t, dt_)
+            self.ctx.aggregate(tables[-1], dt_, outs_, odt)
     offs, padded = layout.padded_offsets(4)
     flat = torch.empty(padded, dtype=torch.float32, device=dev)
     outs = OutputTable([flat[o:o + m] for o, m in zip(offs, layout.numels)], layout, dev, torch.float32)
@@ -61,7 +74,7 @@ def run_all(rounds=7, iters=10):
         ctxs[name] = FedAvgContext(layout, dev, lib=lib)
         if name.endswith("_nofma"):
             ctxs[name].set_fused_fold(False)
-        ctxs[name].aggregate(table, dt, outs, torch.float32)
+        Waves(ctxs[name]).aggregate(table, dt, outs, torch.float32)
         torch.cuda.synchronize()
         if ref is None:
             ref = flat.clone()
@@ -72,11 +85,13 @@ def run_all(rounds=7, iters=10):
         for name, ctx in ctxs.items():
             ctx.prof_enable(True)
             for _ in range(iters):
-                ctx.aggregate(table, dt, outs, torch.float32)
+                Waves(ctx).aggregate(table, dt, outs, torch.float32)
             ctx.prof_enable(False)
             ms, n = ctx.prof_collect()
-            times[name].append(ms / n)
-    nbytes = K * layout.total_numel * buckets.element_size() + layout.total_numel * 4
+            times[name].append(ms / iters)  # kernel ms per job (all its launches)
+    # algorithmic bytes of the job + the fp64 accumulator round trips between waves
+    nbytes = K * layout.total_numel * buckets.element_size() + layout.total_numel * 4 \
+        + (len(tables) - 1) * layout.total_numel * 16
     res = {}
     for name, t in times.items():
         med = float(np.median(t))

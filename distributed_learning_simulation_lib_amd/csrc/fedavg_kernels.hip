@@ -118,6 +118,15 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_PIPE
 #define FEDAVG_PIPE 1
 #endif
+#ifndef FEDAVG_ACC_PLAIN_STORE_HALF  // 2-byte inputs: the fp64 accumulator of a wave is stored with
+// plain (not non-temporal) stores. Interleaved A/B on MI355X: 128 x GPT-2 fp16 in waves of 32
+// 7.61 -> 6.84 ms (+11 %), 64 x ResNet-18 bf16 in waves of 16 +3.5 %, one-launch unchanged; the
+// same for fp32 (all stores plain) cost ViT-B/16 waves 2.4 % (kept non-temporal there)
+#define FEDAVG_ACC_PLAIN_STORE_HALF 1
+#endif
+#ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
+#define FEDAVG_ACC_NT_LOAD 0
+#endif
 #ifndef FEDAVG_PIPE_BYTES  // bytes of client loads per lane per pipeline stage
 #define FEDAVG_PIPE_BYTES 64
 #endif
@@ -468,7 +477,11 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
       for (int j = 0; j < N; j += 2) {
         if (FULL || e + j + 2 <= count) {
+#if FEDAVG_ACC_NT_LOAD
+          const f64x2 d = __builtin_nontemporal_load((gptr<const f64x2>)(ap + e + j));
+#else
           const f64x2 d = *(gptr<const f64x2>)(ap + e + j);
+#endif
           acc[v * N + j] = d.x;
           acc[v * N + j + 1] = d.y;
         } else {
@@ -665,7 +678,12 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
       for (int j = 0; j < N; j += 2) {
         if (FULL || e + j + 2 <= count) {
-          store_out((gptr<f64x2>)(ap + e + j), f64x2{acc[v * N + j], acc[v * N + j + 1]});
+          const f64x2 pair = f64x2{acc[v * N + j], acc[v * N + j + 1]};
+          if constexpr (sizeof(T) == 2 && FEDAVG_ACC_PLAIN_STORE_HALF) {
+            *(gptr<f64x2>)(ap + e + j) = pair;  // see FEDAVG_ACC_PLAIN_STORE_HALF
+          } else {
+            store_out((gptr<f64x2>)(ap + e + j), pair);
+          }
         } else {
           if (e + j < count) ap[e + j] = acc[v * N + j];
           if (e + j + 1 < count) ap[e + j + 1] = acc[v * N + j + 1];

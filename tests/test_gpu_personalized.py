@@ -25,14 +25,15 @@ pytestmark = pytest.mark.gpu
 CASES = load_personalized()
 
 
-def run_hip(case, device, from_host=False):
+def run_hip(case, device, from_host=False, wire=None):
     algo = PersonalizedFedAVGAlgorithm(device=device)
     algo.set_worker_weights({j: dict(v) for j, v in case.worker_weights.items()})
+    msg_cls = ParameterMessage if wire is None else wire.ParameterMessage
     for a in case.arrivals:
         msg = None
         if a.arrays is not None:
-            msg = ParameterMessage(parameter=case.torch_params(a, "cpu" if from_host else device),
-                                   other_data=dict(a.other_data))
+            msg = msg_cls(parameter=case.torch_params(a, "cpu" if from_host else device),
+                          other_data=dict(a.other_data))
         algo.process_worker_data(a.worker_id, msg)
     return algo.aggregate_worker_data()
 
@@ -159,3 +160,21 @@ def test_nan_input_names_the_worker(hip_device):
     with pytest.raises(NaNAggregationError) as ei:
         _hip(clients, ww, hip_device)
     assert ei.value.stage == "input" and ei.value.bad_clients == [3]
+
+
+@pytest.mark.parametrize("name", sorted(n for n in CASES if CASES[n].error is None)[:6])
+def test_personalized_with_foreign_messages(hip_device, name):
+    """Updates of another wire module (the reference server passes simulation_lib.message
+    objects): recognised by their fields; the result is that module's MultipleWorkerMessage of
+    its ParameterMessages (aggregation_server.py:84-86 dispatches on them), bits unchanged."""
+    import tests.foreign_messages as foreign
+
+    case = CASES[name]
+    res = run_hip(case, hip_device, wire=foreign)
+    assert type(res) is foreign.MultipleWorkerMessage
+    for r in case.meta["receivers"]:
+        got = res.worker_data[r["worker_id"]]
+        assert type(got) is foreign.ParameterMessage
+        for k, want in case.expected[r["worker_id"]].items():
+            assert bits_equal(got.parameter[k].cpu().numpy(), want), f"{name}/{r['worker_id']}/{k}"
+

@@ -124,6 +124,12 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 // same for fp32 (all stores plain) cost ViT-B/16 waves 2.4 % (kept non-temporal there)
 #define FEDAVG_ACC_PLAIN_STORE_HALF 1
 #endif
+#ifndef FEDAVG_ACC_PLAIN_STORE_F32  // the same for fp32 / fp64 inputs (A/B knobs)
+#define FEDAVG_ACC_PLAIN_STORE_F32 0
+#endif
+#ifndef FEDAVG_ACC_PLAIN_STORE_F64
+#define FEDAVG_ACC_PLAIN_STORE_F64 0
+#endif
 #ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
 #define FEDAVG_ACC_NT_LOAD 0
 #endif
@@ -679,7 +685,8 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
       for (int j = 0; j < N; j += 2) {
         if (FULL || e + j + 2 <= count) {
           const f64x2 pair = f64x2{acc[v * N + j], acc[v * N + j + 1]};
-          if constexpr (sizeof(T) == 2 && FEDAVG_ACC_PLAIN_STORE_HALF) {
+          if constexpr ((sizeof(T) == 2 && FEDAVG_ACC_PLAIN_STORE_HALF) ||
+                        (sizeof(T) == 4 && FEDAVG_ACC_PLAIN_STORE_F32) || (sizeof(T) == 8 && FEDAVG_ACC_PLAIN_STORE_F64)) {
             *(gptr<f64x2>)(ap + e + j) = pair;  // see FEDAVG_ACC_PLAIN_STORE_HALF
           } else {
             store_out((gptr<f64x2>)(ap + e + j), pair);

@@ -13,8 +13,7 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "accpl_h": {"FEDAVG_ACC_PLAIN_STORE_HALF": 1},
-    "ntst0": {"FEDAVG_NT_STORE": 0},
+    "accpl_all": {"FEDAVG_ACC_PLAIN_STORE_F32": 1, "FEDAVG_ACC_PLAIN_STORE_F64": 1},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

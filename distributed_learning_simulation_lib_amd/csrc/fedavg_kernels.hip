@@ -24,6 +24,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdint>
@@ -129,6 +130,9 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #endif
 #ifndef FEDAVG_ACC_PLAIN_STORE_F64
 #define FEDAVG_ACC_PLAIN_STORE_F64 0
+#endif
+#ifndef FEDAVG_BALANCE_DEFAULT  // balanced whole-layout tile orders (bit 0 fp32, bit 1 fp64); env FEDAVG_BALANCE
+#define FEDAVG_BALANCE_DEFAULT 3
 #endif
 #ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
 #define FEDAVG_ACC_NT_LOAD 0
@@ -334,16 +338,21 @@ struct LaneLoader {
   static constexpr int N = Vec16<T>::n;
   static constexpr int VPL = AE / N;
 
-  // raw 16-B loads (fast path: whole tile, aligned buffers)
-  __device__ __forceinline__ static void load_raw(gptr<const T> base, int li, V (&buf)[VPL]) {
+  // raw 16-B loads (fast path: aligned buffers; a whole tile, or — nv < VPL — a tile of nv
+  // whole lane-vectors, the rest zero: a wave-uniform guard, no per-lane bounds)
+  __device__ __forceinline__ static void load_raw(gptr<const T> base, int li, V (&buf)[VPL], int nv = VPL) {
     const gptr<const V> vb = (gptr<const V>)base;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
+      if (FULL || v < nv) {
 #if FEDAVG_NT
-      buf[v] = __builtin_nontemporal_load(vb + v * LANES + li);
+        buf[v] = __builtin_nontemporal_load(vb + v * LANES + li);
 #else
-      buf[v] = vb[v * LANES + li];
+        buf[v] = vb[v * LANES + li];
 #endif
+      } else {
+        buf[v] = V{};
+      }
     }
   }
 
@@ -434,7 +443,10 @@ __device__ __forceinline__ double fold(double acc, double x, double w, double ba
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD, int TILEN = kTile1>
+// PARTV: a tile shorter than TILE whose count is a whole number of lane-vectors (LANES * N
+// elements): the grouped / pipelined fast path with the missing vectors guarded wave-uniformly
+// (the balanced tile tables end every launch with such tiles, see build_balanced_tiles).
+template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD, int TILEN = kTile1, bool PARTV = false>
 __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
   constexpr int AE = Geo<T, SPLIT, TILEN>::AE;
   constexpr int LANES = Geo<T, SPLIT, TILEN>::LANES;  // lanes sharing one client stream
@@ -445,10 +457,11 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   // clients in flight per lane: 256 B of loads per lane per group
   constexpr int CU_B = sizeof(T) == 8 ? FEDAVG_CU_BYTES_F64 : FEDAVG_CU_BYTES;
   constexpr int CU_LOADS = (CU_B / (VPL * 16)) < 2 ? 2 : (CU_B / (VPL * 16));
-  constexpr bool FAST = FULL && VEC;
+  constexpr bool FAST = (FULL || PARTV) && VEC;
 
   const int seg = td.seg;
   const int count = td.count;
+  const int nv = FULL ? VPL : count / (LANES * N);  // whole lane-vectors of the tile (PARTV)
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int li = (SPLIT == 1) ? static_cast<int>(threadIdx.x) : static_cast<int>(threadIdx.x & 63);
 
@@ -545,7 +558,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
       for (int c = 0; c < PG; ++c) {
         const int kc = min(k + c, ke - 1);
         wk[c] = wp[kc];
-        LL::load_raw(client(kc), li, buf[c]);
+        LL::load_raw(client(kc), li, buf[c], nv);
       }
     };
     auto fold_stage = [&](auto tail_tag, V (&buf)[PG][VPL], const double (&wk)[PG], int n) {
@@ -598,7 +611,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
       for (int c = 0; c < CU_LOADS; ++c) {
         const int kc = TAIL ? k + min(c, n - 1) : k + c;
         wk[c] = wp[kc];
-        LL::load_raw(client(kc), li, buf[c]);
+        LL::load_raw(client(kc), li, buf[c], nv);
       }
 #if FEDAVG_LOAD_FENCE
       __builtin_amdgcn_sched_barrier(0);  // every load of the group issues before any fold
@@ -785,10 +798,17 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
   const int ntiles = (SPLIT == 1) ? a.num_tiles : static_cast<int>(gridDim.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const TileDesc td = load_tile(a.tiles, a.tile_begin + t);
+    constexpr int LV = Geo<T, SPLIT, TILEN>::LANES * Vec16<T>::n;  // elements per lane-vector row
     if (td.count == TILE) {
       tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN>(a, td, lds);
     } else {
-      tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN>(a, td, lds);
+      bool partv = false;
+      if constexpr (SPLIT == 1 && VEC && LV < TILE) partv = (td.count % LV) == 0;
+      if (partv) {
+        if constexpr (SPLIT == 1 && VEC && LV < TILE) tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN, true>(a, td, lds);
+      } else {
+        tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN>(a, td, lds);
+      }
     }
     if constexpr (SPLIT > 1) break;
   }
@@ -1311,6 +1331,11 @@ struct fedavg_ctx {
   TileDesc* d_tiles1 = nullptr;
   TileDesc* d_tiles4 = nullptr;
   TileDesc* d_tilesw = nullptr;
+  // balanced orders of the whole-layout tables (build_balanced_tiles): fp32 on kTileWide tiles,
+  // fp64 on kTile1 tiles; empty = not used (FEDAVG_BALANCE)
+  std::vector<TileDesc> tilesw_bal, tiles1_bal;
+  TileDesc* d_tilesw_bal = nullptr;
+  TileDesc* d_tiles1_bal = nullptr;
   SegDesc* d_segs = nullptr;
   uint32_t* h_flag = nullptr;  // host-coherent pinned NaN words (kernels store into them)
   uint32_t* d_flag = nullptr;  // device alias of h_flag
@@ -1365,6 +1390,54 @@ int32_t elem_size(int32_t dt) {
     case FEDAVG_QSGD_F64: return 1;
     default: return 0;
   }
+}
+
+// A whole-layout launch runs one workgroup per tile and `slots` workgroups at a time (resident
+// workgroups per CU x CUs). With every tile the same length the launch ends with a partial wave
+// (64 x ResNet-18 fp32: 1427 tiles of 8192 = 5.57 waves of 256 — the last 0.57 wave leaves 43 % of
+// the CUs idle; a flat layout of 5.00 / 5.08 waves runs at 6.8 / 6.2 TB/s, scripts/tail_probe.py).
+// The balanced order keeps whole waves of full tiles first, then cuts the remaining full tiles into
+// pieces of whole lane-vectors (`gran` elements, the PARTV fast path) sized so the remaining work
+// spreads over all slots, and ends with those pieces and the segments' tail pieces sorted longest
+// first (list scheduling then finishes the slots within about one piece of each other). Any
+// partition of the elements folds every element identically, so the bits do not change.
+void build_balanced_tiles(const std::vector<int64_t>& numel, int tile, int gran, int64_t slots,
+                          std::vector<TileDesc>& out) {
+  std::vector<TileDesc> full, tail;
+  int64_t tail_elems = 0;
+  for (size_t t = 0; t < numel.size(); ++t) {
+    const int64_t q = numel[t] / tile;
+    for (int64_t i = 0; i < q; ++i) full.push_back(TileDesc{static_cast<int32_t>(t), tile, i * tile});
+    int64_t start = q * tile, r = numel[t] - q * tile;
+    const int64_t rv = r - r % gran;  // whole lane-vectors: fast path
+    if (rv > 0) {
+      tail.push_back(TileDesc{static_cast<int32_t>(t), static_cast<int32_t>(rv), start});
+      start += rv;
+      r -= rv;
+      tail_elems += rv;
+    }
+    if (r > 0) {
+      tail.push_back(TileDesc{static_cast<int32_t>(t), static_cast<int32_t>(r), start});
+      tail_elems += r;
+    }
+  }
+  slots = std::max<int64_t>(slots, 1);
+  const int64_t head = (static_cast<int64_t>(full.size()) / slots) * slots;
+  const int64_t rest = static_cast<int64_t>(full.size()) - head;
+  const int64_t remaining = rest * tile + tail_elems;
+  int64_t piece = (remaining + slots - 1) / slots;
+  piece = std::min<int64_t>(tile, std::max<int64_t>(gran, (piece + gran - 1) / gran * gran));
+  out.assign(full.begin(), full.begin() + head);
+  std::vector<TileDesc> end;
+  for (int64_t i = head; i < static_cast<int64_t>(full.size()); ++i) {
+    for (int64_t s = 0; s < tile; s += piece) {
+      const int64_t c = std::min<int64_t>(piece, tile - s);
+      end.push_back(TileDesc{full[i].seg, static_cast<int32_t>(c), full[i].start + s});
+    }
+  }
+  end.insert(end.end(), tail.begin(), tail.end());
+  std::stable_sort(end.begin(), end.end(), [](const TileDesc& a, const TileDesc& b) { return a.count > b.count; });
+  out.insert(out.end(), end.begin(), end.end());
 }
 
 void build_tiles(const std::vector<int64_t>& numel, int tile, std::vector<TileDesc>& out) {
@@ -1704,6 +1777,15 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     a.tiles = c->d_tilesw;
     tb = 0;
     te = static_cast<int>(c->tilesw.size());
+    if (in_dtype == FEDAVG_F32 && c->d_tilesw_bal != nullptr) {
+      a.tiles = c->d_tilesw_bal;
+      te = static_cast<int>(c->tilesw_bal.size());
+    }
+  } else if (split == 1 && in_dtype == FEDAVG_F64 && c->d_tiles1_bal != nullptr && c->persistent_blocks == 0 &&
+             tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
+    a.tiles = c->d_tiles1_bal;  // a whole-layout fp64 launch: the balanced order of the same tiles
+    tb = 0;
+    te = static_cast<int>(c->tiles1_bal.size());
   }
   a.tile_begin = tb;
   a.num_tiles = te - tb;
@@ -1854,6 +1936,29 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);
   if (kTileWide > 0) build_tiles(c->seg_numel, kTileWide, c->tilesw);
+  {
+    // balanced whole-layout orders (FEDAVG_BALANCE bit 0: fp32 on the wide table, bit 1: fp64 on
+    // the kTile1 table), sized by the resident workgroups of the kernel that runs them
+    const char* env = std::getenv("FEDAVG_BALANCE");
+    const int bal = env ? std::atoi(env) : FEDAVG_BALANCE_DEFAULT;
+    int cus = 0;
+    if (bal && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
+      int per_cu = 0;
+      if ((bal & 1) && kTileWide > 0 &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA, kTileWide>),
+              Geo<float, 1, kTileWide>::THREADS, 0) == hipSuccess && per_cu > 0)
+        build_balanced_tiles(c->seg_numel, kTileWide, Geo<float, 1, kTileWide>::LANES * Vec16<float>::n,
+                             static_cast<int64_t>(per_cu) * cus, c->tilesw_bal);
+      per_cu = 0;
+      if ((bal & 2) &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<double, OUT_F32, 1, true, FOLD_FMA, kTile1>),
+              Geo<double, 1, kTile1>::THREADS, 0) == hipSuccess && per_cu > 0)
+        build_balanced_tiles(c->seg_numel, kTile1, Geo<double, 1, kTile1>::LANES * Vec16<double>::n,
+                             static_cast<int64_t>(per_cu) * cus, c->tiles1_bal);
+    }
+  }
 #if FEDAVG_PERSISTENT
   {
     int per_cu = 0, cus = 0;
@@ -1903,6 +2008,13 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   }
   if ((e = hipMemcpy(c->d_segs, segs.data(), sizeof(SegDesc) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "hipMemcpy segs");
+  for (auto [host, dev] : {std::pair{&c->tilesw_bal, &c->d_tilesw_bal}, std::pair{&c->tiles1_bal, &c->d_tiles1_bal}}) {
+    if (host->empty()) continue;
+    if ((e = hipMalloc(reinterpret_cast<void**>(dev), sizeof(TileDesc) * host->size())) != hipSuccess)
+      return cleanup(e, "hipMalloc balanced tiles");
+    if ((e = hipMemcpy(*dev, host->data(), sizeof(TileDesc) * host->size(), hipMemcpyHostToDevice)) != hipSuccess)
+      return cleanup(e, "hipMemcpy balanced tiles");
+  }
   std::memset(c->h_flag, 0, sizeof(uint32_t) * 4);
   if (accumulator != nullptr) {
     c->acc = static_cast<double*>(accumulator);
@@ -1935,6 +2047,8 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   if (c->d_tiles1) (void)hipFree(c->d_tiles1);
   if (c->d_tiles4) (void)hipFree(c->d_tiles4);
   if (c->d_tilesw) (void)hipFree(c->d_tilesw);
+  if (c->d_tilesw_bal) (void)hipFree(c->d_tilesw_bal);
+  if (c->d_tiles1_bal) (void)hipFree(c->d_tiles1_bal);
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->owns_acc && c->acc) (void)hipFree(c->acc);

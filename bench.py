@@ -50,7 +50,9 @@ from distributed_learning_simulation_lib_amd.fedavg import (  # noqa: E402
 from distributed_learning_simulation_lib_amd.sharded import (  # noqa: E402
     HipLocalReducer,
     RcclComm,
+    exchange_candidates,
     resolve_exchange,
+    tune_exchange,
     sharded_reduce,
 )
 
@@ -548,7 +550,11 @@ def main() -> int:
                          "call (native) or the chunks' reduces through torch.distributed (torch)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "reduce", "scatter"],
                     help="multi-GPU exchange of the fp64 partials: reduce to rank 0, or reduce-scatter + "
-                         "per-rank finalize + gather (auto: scatter at 2 ranks, reduce above; DESIGN.md §5)")
+                         "per-rank finalize + gather (auto: the fastest (exchange, chunks) pair timed on the "
+                         "node before the warmup; with --no-tune scatter at 2 ranks, reduce above; DESIGN.md §5)")
+    ap.add_argument("--no-tune", action="store_true",
+                    help="N > 1 with --exchange auto: take the cost model's exchange instead of timing "
+                         "every (exchange, chunks) candidate before the warmup")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
     ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -584,7 +590,8 @@ def main() -> int:
         opts.is_high_priority_stream = True
         dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world, pg_options=opts)
     sharded = world > 1 or args.force_collective
-    if args.chunks <= 0:
+    chunks_auto = args.chunks <= 0
+    if chunks_auto:
         args.chunks = 4 if world > 1 else 2
 
     in_dtype = getattr(torch, args.in_dtype)
@@ -637,6 +644,17 @@ def main() -> int:
             args.comm = "torch"
 
     exchange = resolve_exchange(args.exchange, world)
+    selection = "fixed" if args.exchange != "auto" else "cost model"
+    tuned = None
+    if sharded and args.exchange == "auto" and not args.no_tune:
+        # time every (exchange, chunks) candidate on this node before the warmup (untimed; the
+        # max over ranks decides, so every rank picks the same): the link rate the DESIGN.md §5
+        # cost model assumes is not measurable on one GPU
+        (exchange, args.chunks), times = tune_exchange(
+            reducer, local_totals, exchange_candidates(None if chunks_auto else args.chunks), rounds=3,
+            global_total_weights=global_totals, comm=comm)
+        tuned = {f"{e}/{c}": round(ms, 4) for (e, c), ms in times.items()}
+        selection = "tuned"
 
     def step() -> None:
         h0 = time.perf_counter()
@@ -787,7 +805,8 @@ def main() -> int:
                 f"clients sharded over {world} GPUs + chunked RCCL "
                 + ("reduce to rank 0" if exchange == "reduce" else "reduce-scatter, per-rank finalize, gather to rank 0")),
             "exchange": None if not sharded else {
-                "mode": exchange, "chunks": args.chunks, "comm": args.comm,
+                "mode": exchange, "chunks": args.chunks, "comm": args.comm, "selection": selection,
+                "tuned_ms_per_round": tuned,
                 "partial_only_ms_per_step": None if partial_only_ms is None else round(partial_only_ms, 4),
                 "exposed_exchange_and_finalize_ms": (None if partial_only_ms is None
                                                      else round(step_s * 1e3 - partial_only_ms, 4)),

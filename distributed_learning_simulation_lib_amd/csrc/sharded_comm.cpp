@@ -122,6 +122,9 @@ struct fedavg_comm {
   int32_t rank = 0;
   int32_t device = 0;
   hipStream_t stream = nullptr;  // high-priority comm stream
+  // the root's last step (finalize / copy-out) runs on the comm stream right behind the last
+  // collective instead of on the compute stream behind a cross-stream wait (FEDAVG_FINISH_ON_COMM)
+  bool finish_on_comm = false;
   std::vector<hipEvent_t> chunk_events;
   hipEvent_t done = nullptr;
   // scatter exchange scratch: reduce-scattered fp64 windows (+ the root's chunk tails) and the
@@ -206,6 +209,7 @@ int32_t fedavg_comm_create(fedavg_comm** out, const void* id, int32_t world, int
   c->world = world;
   c->rank = rank;
   c->device = device;
+  if (const char* e = std::getenv("FEDAVG_FINISH_ON_COMM")) c->finish_on_comm = std::atoi(e) != 0;
   int lo = 0, hi = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
   if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
@@ -279,10 +283,12 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
   // root then divides every tile in one launch. (Dividing each chunk on the comm stream right
   // behind its reduce was measured slower: 0.595 vs 0.566 ms per one-rank round at 4 chunks —
   // the finalize kernels contend with the next chunk's partial for CUs and HBM.)
+  fedavg_internal_set_prof(ctx, 0);
+  if (c->rank == root && c->finish_on_comm)
+    if (int32_t st = fedavg_plan_run_range(finalize, 0, n, c->stream)) return st;
   COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
   COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
-  fedavg_internal_set_prof(ctx, 0);
-  if (c->rank == root) return fedavg_plan_run_range(finalize, 0, n, s);
+  if (c->rank == root && !c->finish_on_comm) return fedavg_plan_run_range(finalize, 0, n, s);
   return FEDAVG_OK;
 }
 
@@ -365,10 +371,12 @@ int32_t fedavg_sharded_round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_pla
       if (res != ncclSuccess) return rccl_fail(res, "ncclGather");
     }
   }
+  fedavg_internal_set_prof(ctx, 0);
+  if (c->rank == root && c->finish_on_comm)
+    if (int32_t st = fedavg_plan_copy_out(finalize, c->res, c->stream)) return st;
   COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
   COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
-  fedavg_internal_set_prof(ctx, 0);
-  if (c->rank == root) return fedavg_plan_copy_out(finalize, c->res, s);
+  if (c->rank == root && !c->finish_on_comm) return fedavg_plan_copy_out(finalize, c->res, s);
   return FEDAVG_OK;
 }
 

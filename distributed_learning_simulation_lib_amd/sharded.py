@@ -19,7 +19,9 @@ cost table), both the one exchange step of the path:
     to the root, which copies them into its outputs. Root ingress (G-1)/G x (fp64 partial +
     result) instead of the whole fp64 partial; all ranks do equal exchange work.
 
-``exchange="auto"`` picks scatter at 2 ranks and reduce above (the cost model of DESIGN.md §5).
+``exchange="auto"`` picks scatter at 2 ranks and reduce above (the cost model of DESIGN.md §5);
+``tune_exchange`` instead times every (exchange, chunks) candidate on the live job and returns
+the fastest, the same answer on every rank.
 A process group on the ``gloo`` backend with GPU accumulators stages each chunk through host
 memory (tests and hosts without RCCL); ``nccl`` (= RCCL) works on HBM directly.
 
@@ -36,6 +38,7 @@ chunking / collective / finalize logic without a GPU.
 from __future__ import annotations
 
 import ctypes
+import time
 from collections.abc import Sequence
 from typing import Protocol
 
@@ -157,7 +160,6 @@ class HipLocalReducer:
                 flat = torch.empty(total, dtype=self.out_dtype, device=self.ctx.device)
                 self.outs = OutputTable([flat[o : o + m] for o, m in zip(offs, self.ctx.layout.numels)],
                                         self.ctx.layout, self.ctx.device, self.out_dtype)
-                self._scratch_outs = True
             self._finalize_plan = self.ctx.plan_finalize(totals, self.outs, self.out_dtype)
             self._finalize_totals = totals
 
@@ -319,6 +321,66 @@ def sharded_reduce(
     if check_nan and rank == root:
         reducer.raise_on_nan()
     return global_totals
+
+
+def exchange_candidates(chunks: int | None = None) -> list[tuple[str, int]]:
+    """(exchange, chunks) pairs ``tune_exchange`` tries: both exchanges at 2 / 4 / 8 chunks, or
+    at the given chunk count only."""
+    return [(ex, c) for ex in ("reduce", "scatter") for c in ((chunks,) if chunks else (2, 4, 8))]
+
+
+def tune_exchange(
+    reducer: LocalReducer,
+    local_total_weights: Sequence[float],
+    candidates: Sequence[tuple[str, int]] | None = None,
+    rounds: int = 3,
+    root: int = 0,
+    group: dist.ProcessGroup | None = None,
+    global_total_weights: Sequence[float] | None = None,
+    comm: RcclComm | None = None,
+    force_collective: bool = False,
+) -> tuple[tuple[str, int], dict[tuple[str, int], float]]:
+    """Pick the exchange and chunk count by timing the job itself.
+
+    The cost model of DESIGN.md §5 rests on a link rate no single-GPU box can measure, so the
+    multi-GPU round can instead be tuned on the node it runs on: each candidate runs one
+    untimed round (plans and scratch), then ``rounds`` rounds between a barrier and a device
+    sync; the time of a candidate is the max over ranks (one all-reduce), so every rank ranks
+    the candidates identically and returns the same choice. Ties go to the earlier candidate.
+    Returns ``((exchange, chunks), {candidate: ms per round})``. Collective: every rank of
+    ``group`` calls it with the same candidates.
+    """
+    cands = list(candidates) if candidates is not None else exchange_candidates()
+    if not cands:
+        raise ValueError("no candidates to tune")
+    for ex, ch in cands:
+        resolve_exchange(ex, 2)
+        if ch < 1:
+            raise ValueError(f"chunks must be >= 1, not {ch}")
+    acc = reducer.accumulator
+    on_host = not acc.is_cuda or dist.get_backend(group) == "gloo"
+
+    def settle() -> None:
+        if acc.is_cuda:
+            torch.cuda.synchronize(acc.device)
+
+    times: dict[tuple[str, int], float] = {}
+    for ex, ch in cands:
+        kw = dict(chunks=ch, root=root, group=group, global_total_weights=global_total_weights,
+                  force_collective=force_collective, comm=comm, exchange=ex, check_nan=False)
+        sharded_reduce(reducer, local_total_weights, **kw)
+        settle()
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(max(1, rounds)):
+            sharded_reduce(reducer, local_total_weights, **kw)
+        settle()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device="cpu" if on_host else acc.device)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
+        times[(ex, ch)] = float(el.item()) / max(1, rounds) * 1e3
+    best = min(range(len(cands)), key=lambda i: (times[cands[i]], i))
+    return cands[best], times
 
 
 def _reduce_exchange(reducer: LocalReducer, global_totals: list[float], chunks: int, rank: int, root: int,

@@ -215,6 +215,55 @@ def test_root_raises_on_a_nan_in_another_shard(exchange):
     assert got[0] == "AssertionError"  # the root sees the NaN (fed_avg_algorithm.py:35/93/97)
 
 
+def _tune_worker(rank, world, port, q):
+    from distributed_learning_simulation_lib_amd.sharded import exchange_candidates, tune_exchange
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        clients, weights = make_all_clients(5)
+        mine = [i for i in range(5) if i % world == rank]
+        outs = [torch.empty(m, dtype=torch.float64) for m in LAYOUT.numels] if rank == 0 else None
+        red = TorchCPUReducer(LAYOUT, [clients[i] for i in mine], [weights[i] for i in mine], outs)
+        local = [sum(weights[i][s] for i in mine) for s in range(LAYOUT.num_segments)]
+        (ex, ch), times = tune_exchange(red, local, exchange_candidates(), rounds=2)
+        sharded_reduce(red, local, chunks=ch, exchange=ex)  # the tuned round still aggregates
+        q.put((rank, (ex, ch), sorted(times), [o.numpy() for o in outs] if rank == 0 else None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tune_exchange_agrees_across_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: (choice, timed, outs) for r, choice, timed, outs in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from distributed_learning_simulation_lib_amd.sharded import exchange_candidates
+
+    assert got[0][0] == got[1][0]  # max-over-ranks times: one answer everywhere
+    assert got[0][1] == sorted(exchange_candidates()) and got[0][0] in exchange_candidates()
+    clients, weights = make_all_clients(5)
+    for s in range(LAYOUT.num_segments):
+        want = fedavg_flat([c[s].numpy() for c in clients], [w[s] for w in weights])
+        mag = sum(np.abs(c[s].numpy().astype(np.float64)) * w[s] for c, w in zip(clients, weights)) / sum(
+            w[s] for w in weights)
+        assert np.all(np.abs(got[0][2][s] - want) <= 1e-12 * mag)
+
+
+def test_exchange_candidates():
+    from distributed_learning_simulation_lib_amd.sharded import exchange_candidates
+
+    assert exchange_candidates(4) == [("reduce", 4), ("scatter", 4)]
+    assert len(exchange_candidates()) == 6
+
+
 def test_resolve_exchange():
     from distributed_learning_simulation_lib_amd.sharded import resolve_exchange, scatter_windows
 

@@ -652,7 +652,7 @@ def main() -> int:
         # cost model assumes is not measurable on one GPU
         (exchange, args.chunks), times = tune_exchange(
             reducer, local_totals, exchange_candidates(None if chunks_auto else args.chunks), rounds=3,
-            global_total_weights=global_totals, comm=comm)
+            global_total_weights=global_totals, comm=comm, force_collective=args.force_collective)
         tuned = {f"{e}/{c}": round(ms, 4) for (e, c), ms in times.items()}
         selection = "tuned"
 

@@ -339,6 +339,7 @@ def tune_exchange(
     global_total_weights: Sequence[float] | None = None,
     comm: RcclComm | None = None,
     force_collective: bool = False,
+    check_nan: bool = True,
 ) -> tuple[tuple[str, int], dict[tuple[str, int], float]]:
     """Pick the exchange and chunk count by timing the job itself.
 
@@ -346,7 +347,10 @@ def tune_exchange(
     multi-GPU round can instead be tuned on the node it runs on: each candidate runs one
     untimed round (plans and scratch), then ``rounds`` rounds between a barrier and a device
     sync; the time of a candidate is the max over ranks (one all-reduce), so every rank ranks
-    the candidates identically and returns the same choice. Ties go to the earlier candidate.
+    the candidates identically and returns the same choice. Each round ends as a server's does,
+    with the root reading the NaN flags (``check_nan``): without that host sync, back-to-back
+    rounds overlap one round's exchange with the next round's fold, a pipelining no
+    round-by-round server gets, and the candidates would be ranked on it. Ties go to the earlier candidate.
     Returns ``((exchange, chunks), {candidate: ms per round})``. Collective: every rank of
     ``group`` calls it with the same candidates.
     """
@@ -367,7 +371,7 @@ def tune_exchange(
     times: dict[tuple[str, int], float] = {}
     for ex, ch in cands:
         kw = dict(chunks=ch, root=root, group=group, global_total_weights=global_total_weights,
-                  force_collective=force_collective, comm=comm, exchange=ex, check_nan=False)
+                  force_collective=force_collective, comm=comm, exchange=ex, check_nan=check_nan)
         sharded_reduce(reducer, local_total_weights, **kw)
         settle()
         dist.barrier(group=group)

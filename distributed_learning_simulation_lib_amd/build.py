@@ -23,7 +23,13 @@ SOURCES = [CSRC / "fedavg_kernels.hip", CSRC / "personalized_kernels.hip", CSRC 
            CSRC / "sharded_comm.cpp"]
 HEADERS = [REPO_DIR / "include" / "fedavg_hip.h"]
 # C++ clients of the ABI alone (no Python, no torch), built next to the library
-EXAMPLES = {"c_abi_round": REPO_DIR / "examples" / "c_abi_round.cpp"}
+EXAMPLES = {"c_abi_round": REPO_DIR / "examples" / "c_abi_round.cpp",
+            # test infrastructure: the native multi-rank round with ranks as threads on one GPU
+            "threaded_ranks": REPO_DIR / "tests" / "native" / "threaded_ranks.cpp"}
+# test infrastructure: in-process RCCL stand-ins for threaded_ranks (tests/native/fake_rccl.cpp),
+# with ncclGather and without it (the grouped send / recv fallback of sharded_comm.cpp)
+FAKE_RCCL_SRC = REPO_DIR / "tests" / "native" / "fake_rccl.cpp"
+FAKE_RCCL = {"libfake_rccl.so": [], "libfake_rccl_nogather.so": ["-DFAKE_RCCL_NO_GATHER"]}
 
 # -ffp-contract=off: the reference rounds the fp64 product and the fp64 sum separately
 # (torch `x.to(f64) * w` then `acc += tmp`); an FMA would change low bits.
@@ -76,21 +82,31 @@ def build(force: bool = False, verbose: bool = False, defines: dict[str, int] | 
     return target
 
 
+def _run(cmd: list[str], what: str, verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd))
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {what} ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
+
+
 def build_examples(verbose: bool = False) -> list[Path]:
-    """Link each example against the in-tree library (rpath $ORIGIN: they live in _lib/)."""
+    """Link each example against the in-tree library (rpath $ORIGIN: they live in _lib/), and
+    build the test-only RCCL stand-ins."""
     built = []
+    for name, extra in FAKE_RCCL.items():
+        so = LIB_DIR / name
+        if not (so.exists() and so.stat().st_mtime > FAKE_RCCL_SRC.stat().st_mtime):
+            _run([hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", *extra, str(FAKE_RCCL_SRC), "-o", str(so)],
+                 FAKE_RCCL_SRC.name, verbose)
+        built.append(so)
     for name, src in EXAMPLES.items():
         exe = LIB_DIR / name
         if exe.exists() and exe.stat().st_mtime > max(src.stat().st_mtime, LIB_PATH.stat().st_mtime):
             built.append(exe)
             continue
-        cmd = [hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", f"-I{REPO_DIR / 'include'}", str(src),
-               f"-L{LIB_DIR}", "-lfedavg_hip", "-Wl,-rpath,$ORIGIN", "-o", str(exe)]
-        if verbose:
-            print(" ".join(cmd))
-        proc = subprocess.run(cmd, capture_output=True, text=True)
-        if proc.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {src.name} ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
+        _run([hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", f"-I{REPO_DIR / 'include'}", str(src),
+              f"-L{LIB_DIR}", "-lfedavg_hip", "-pthread", "-Wl,-rpath,$ORIGIN", "-o", str(exe)], src.name, verbose)
         built.append(exe)
     return built
 

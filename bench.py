@@ -552,6 +552,9 @@ def main() -> int:
                     help="multi-GPU exchange of the fp64 partials: reduce to rank 0, or reduce-scatter + "
                          "per-rank finalize + gather (auto: the fastest (exchange, chunks) pair timed on the "
                          "node before the warmup; with --no-tune scatter at 2 ranks, reduce above; DESIGN.md §5)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N > 1 on a one-GPU box: all ranks on cuda:0 over gloo (host-staged exchange); "
+                         "exercises the multi-rank code path, not a measurement")
     ap.add_argument("--no-tune", action="store_true",
                     help="N > 1 with --exchange auto: take the cost model's exchange instead of timing "
                          "every (exchange, chunks) candidate before the warmup")
@@ -579,9 +582,17 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    device = torch.device("cuda", local_rank)
+    # --rehearse: every rank on cuda:0 over a gloo group (the exchange staged through host memory,
+    # RCCL refuses two ranks on one GPU) — runs this N > 1 code path on a one-GPU box; its times
+    # are not the N-GPU numbers
+    device = torch.device("cuda", 0 if args.rehearse else local_rank)
     torch.cuda.set_device(device)
-    if world > 1 or args.force_collective:
+    if args.rehearse and (world > 1 or args.force_collective):
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        args.comm = "torch"
+    elif world > 1 or args.force_collective:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         # RCCL on a high-priority stream: its workgroups take free CU slots ahead of the next
@@ -689,7 +700,7 @@ def main() -> int:
     ctx.prof_enable(False)
     kernel_ms, launches = ctx.prof_collect()
     if dist.is_initialized():
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.rehearse else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -737,7 +748,7 @@ def main() -> int:
         torch.cuda.synchronize(device)
         p_el = time.perf_counter() - p0
         if dist.is_initialized():
-            pt = torch.tensor([p_el], dtype=torch.float64, device=device)
+            pt = torch.tensor([p_el], dtype=torch.float64, device="cpu" if args.rehearse else device)
             dist.all_reduce(pt, op=dist.ReduceOp.MAX)
             p_el = float(pt.item())
         partial_only_ms = p_el / args.steps * 1e3
@@ -812,6 +823,8 @@ def main() -> int:
                                                      else round(step_s * 1e3 - partial_only_ms, 4)),
             },
             "baseline_config": baseline_config,
+            **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not an N-GPU measurement"}
+               if args.rehearse else {}),
         },
         "roofline": {
             "bound": "hbm",

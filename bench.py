@@ -520,7 +520,7 @@ def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -
     rocprofv3 PMC summary (scripts/profile.sh -> profiles/<tag>_traffic.json), or None."""
     if world != 1 or n_local != 64 or in_dtype != "float32" or out_dtype != "float32":
         return None, None
-    files = sorted((REPO / "profiles").glob("r*_traffic.json"))
+    files = sorted((REPO / "profiles").glob("r[0-9][0-9]_traffic.json"))  # not the per-config r*_traffic_cfg*
     if not files:
         return None, None
     d = json.loads(files[-1].read_text())

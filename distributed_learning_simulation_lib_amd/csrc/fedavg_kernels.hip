@@ -76,8 +76,12 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_AE
 #define FEDAVG_AE 16
 #endif
-#ifndef FEDAVG_AE_HALF  // elements per lane for 2-byte inputs (fp16 / bf16)
-#define FEDAVG_AE_HALF 8
+#ifndef FEDAVG_AE_HALF  // elements per lane for 2-byte inputs (fp16 / bf16): 16 = two 16-B loads
+// per client per lane, 512-lane wide tiles (interleaved A/B on MI355X against 8: 64 x ResNet-18
+// fp16 one launch 0.2643 -> 0.2472 / 0.2644 -> 0.2488 ms on two boxes, 128 x GPT-2 fp16 one
+// launch 5.420 -> 5.295 / 5.223 -> 5.192 ms, GPT-2 waves of 32 +0.2-0.4 %, ResNet-18 bf16 waves
+// of 16 -1 %; 32 elements per lane and 96 / 128-B pipeline stages mixed)
+#define FEDAVG_AE_HALF 16
 #endif
 #ifndef FEDAVG_AE_F64  // elements per lane for fp64 inputs (8: 512-lane tiles, see CU_BYTES_F64)
 #define FEDAVG_AE_F64 8

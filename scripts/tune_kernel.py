@@ -13,7 +13,11 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "accpl_all": {"FEDAVG_ACC_PLAIN_STORE_F32": 1, "FEDAVG_ACC_PLAIN_STORE_F64": 1},
+    "ae16h": {"FEDAVG_AE_HALF": 16},
+    "ae16h_p128": {"FEDAVG_AE_HALF": 16, "FEDAVG_PIPE_BYTES": 128},
+    "ae16h_p96": {"FEDAVG_AE_HALF": 16, "FEDAVG_PIPE_BYTES": 96},
+    "ae32h_p64": {"FEDAVG_AE_HALF": 32, "FEDAVG_PIPE_BYTES": 64},
+    "ae32h_p128": {"FEDAVG_AE_HALF": 32, "FEDAVG_PIPE_BYTES": 128},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

@@ -13,11 +13,6 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "ae16h": {"FEDAVG_AE_HALF": 16},
-    "ae16h_p128": {"FEDAVG_AE_HALF": 16, "FEDAVG_PIPE_BYTES": 128},
-    "ae16h_p96": {"FEDAVG_AE_HALF": 16, "FEDAVG_PIPE_BYTES": 96},
-    "ae32h_p64": {"FEDAVG_AE_HALF": 32, "FEDAVG_PIPE_BYTES": 64},
-    "ae32h_p128": {"FEDAVG_AE_HALF": 32, "FEDAVG_PIPE_BYTES": 128},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

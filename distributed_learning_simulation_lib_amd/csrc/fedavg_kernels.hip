@@ -141,6 +141,9 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
 #define FEDAVG_ACC_NT_LOAD 0
 #endif
+#ifndef FEDAVG_WALK_ALTERNATE  // streaming waves alternate their tile walk (env FEDAVG_WALK_ALTERNATE)
+#define FEDAVG_WALK_ALTERNATE 1
+#endif
 #ifndef FEDAVG_PIPE_BYTES  // bytes of client loads per lane per pipeline stage
 #define FEDAVG_PIPE_BYTES 64
 #endif
@@ -191,6 +194,8 @@ struct KArgs {
   int32_t num_tiles;   // tiles of this launch (persistent grid-stride bound)
   int32_t K;           // row stride of the [T][K] tables
   int32_t zero_init;   // start every segment at the identity -0.0, ignore acc_in (shard partials)
+  int32_t walk_back;   // the first walk_back tiles of the launch are walked last to first
+                       // (fedavg_ctx::walk_reverse); 0 = natural order
 };
 
 enum OutKind : int { OUT_ACC = 0, OUT_F32 = 1, OUT_F64 = 2 };
@@ -801,7 +806,7 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
   // tile per workgroup (its LDS combine ends with the non-zero waves leaving).
   const int ntiles = (SPLIT == 1) ? a.num_tiles : static_cast<int>(gridDim.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const TileDesc td = load_tile(a.tiles, a.tile_begin + t);
+    const TileDesc td = load_tile(a.tiles, a.tile_begin + (t < a.walk_back ? a.walk_back - 1 - t : t));
     constexpr int LV = Geo<T, SPLIT, TILEN>::LANES * Vec16<T>::n;  // elements per lane-vector row
     if (td.count == TILE) {
       tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN>(a, td, lds);
@@ -1338,6 +1343,7 @@ struct fedavg_ctx {
   // balanced orders of the whole-layout tables (build_balanced_tiles): fp32 on kTileWide tiles,
   // fp64 on kTile1 tiles; empty = not used (FEDAVG_BALANCE)
   std::vector<TileDesc> tilesw_bal, tiles1_bal;
+  int32_t tilesw_bal_head = 0, tiles1_bal_head = 0;  // their leading whole waves of full tiles
   TileDesc* d_tilesw_bal = nullptr;
   TileDesc* d_tiles1_bal = nullptr;
   SegDesc* d_segs = nullptr;
@@ -1368,6 +1374,11 @@ struct fedavg_ctx {
   // whole-layout launches use the wide tile table only when they fold at least this many clients
   // per segment (short waves keep the 4096-element tiles: two workgroups per CU instead of one)
   int wide_min_clients = 0;
+  // Streaming waves alternate the direction they walk the whole layout: a wave that reads the
+  // accumulator starts with the tiles the previous wave wrote last, which are still in L2 / the
+  // memory-side cache. Any tile order folds every element identically (FEDAVG_WALK_ALTERNATE).
+  bool walk_alternate = FEDAVG_WALK_ALTERNATE != 0;
+  bool walk_reverse = false;
   // profiling
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -1405,8 +1416,9 @@ int32_t elem_size(int32_t dt) {
 // spreads over all slots, and ends with those pieces and the segments' tail pieces sorted longest
 // first (list scheduling then finishes the slots within about one piece of each other). Any
 // partition of the elements folds every element identically, so the bits do not change.
-void build_balanced_tiles(const std::vector<int64_t>& numel, int tile, int gran, int64_t slots,
-                          std::vector<TileDesc>& out) {
+// Returns the number of leading full tiles (whole waves).
+int32_t build_balanced_tiles(const std::vector<int64_t>& numel, int tile, int gran, int64_t slots,
+                             std::vector<TileDesc>& out) {
   std::vector<TileDesc> full, tail;
   int64_t tail_elems = 0;
   for (size_t t = 0; t < numel.size(); ++t) {
@@ -1442,6 +1454,7 @@ void build_balanced_tiles(const std::vector<int64_t>& numel, int tile, int gran,
   end.insert(end.end(), tail.begin(), tail.end());
   std::stable_sort(end.begin(), end.end(), [](const TileDesc& a, const TileDesc& b) { return a.count > b.count; });
   out.insert(out.end(), end.begin(), end.end());
+  return static_cast<int32_t>(head);
 }
 
 void build_tiles(const std::vector<int64_t>& numel, int tile, std::vector<TileDesc>& out) {
@@ -1760,6 +1773,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   a.flag = c->d_flag;
   a.K = st.stride;
   a.zero_init = zero_init;
+  a.walk_back = 0;
   int tb = 0, te = 0;
   if (split == 4) {
     // whole-layout launches only (tile ranges are defined on the SPLIT=1 table)
@@ -1794,6 +1808,17 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   a.tile_begin = tb;
   a.num_tiles = te - tb;
   if (a.num_tiles <= 0) return FEDAVG_OK;
+  // whole-layout waves alternate their walk (a balanced order reverses only its leading whole
+  // waves: its short pieces stay at the end, where they balance the tail; ranged launches keep
+  // their order)
+  if (c->walk_alternate && split == 1 && c->persistent_blocks == 0 && !is_qsgd(in_dtype) &&
+      tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
+    if (c->walk_reverse)
+      a.walk_back = (a.tiles == c->d_tilesw_bal)   ? c->tilesw_bal_head
+                    : (a.tiles == c->d_tiles1_bal) ? c->tiles1_bal_head
+                                                   : a.num_tiles;
+    if (out_kind == OUT_ACC) c->walk_reverse = !c->walk_reverse;
+  }
   // exact-order kernel: persistent grid of at most (resident blocks) workgroups
   const int nblocks = (split == 1 && c->persistent_blocks > 0) ? std::min(a.num_tiles, c->persistent_blocks)
                                                                : a.num_tiles;
@@ -1936,6 +1961,7 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   c->acc_numel = off;
   c->wsum.assign(num_segments, -0.0);  // additive identity: the first weight is taken as is
   if (const char* e = std::getenv("FEDAVG_WIDE_MIN_CLIENTS")) c->wide_min_clients = std::atoi(e);
+  if (const char* e = std::getenv("FEDAVG_WALK_ALTERNATE")) c->walk_alternate = std::atoi(e) != 0;
   c->valid.assign(num_segments, 0);
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);
@@ -1952,15 +1978,17 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
           hipOccupancyMaxActiveBlocksPerMultiprocessor(
               &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA, kTileWide>),
               Geo<float, 1, kTileWide>::THREADS, 0) == hipSuccess && per_cu > 0)
-        build_balanced_tiles(c->seg_numel, kTileWide, Geo<float, 1, kTileWide>::LANES * Vec16<float>::n,
-                             static_cast<int64_t>(per_cu) * cus, c->tilesw_bal);
+        c->tilesw_bal_head =
+            build_balanced_tiles(c->seg_numel, kTileWide, Geo<float, 1, kTileWide>::LANES * Vec16<float>::n,
+                                 static_cast<int64_t>(per_cu) * cus, c->tilesw_bal);
       per_cu = 0;
       if ((bal & 2) &&
           hipOccupancyMaxActiveBlocksPerMultiprocessor(
               &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<double, OUT_F32, 1, true, FOLD_FMA, kTile1>),
               Geo<double, 1, kTile1>::THREADS, 0) == hipSuccess && per_cu > 0)
-        build_balanced_tiles(c->seg_numel, kTile1, Geo<double, 1, kTile1>::LANES * Vec16<double>::n,
-                             static_cast<int64_t>(per_cu) * cus, c->tiles1_bal);
+        c->tiles1_bal_head =
+            build_balanced_tiles(c->seg_numel, kTile1, Geo<double, 1, kTile1>::LANES * Vec16<double>::n,
+                                 static_cast<int64_t>(per_cu) * cus, c->tiles1_bal);
     }
   }
 #if FEDAVG_PERSISTENT

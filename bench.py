@@ -50,6 +50,7 @@ from distributed_learning_simulation_lib_amd.fedavg import (  # noqa: E402
 from distributed_learning_simulation_lib_amd.sharded import (  # noqa: E402
     HipLocalReducer,
     RcclComm,
+    chunk_edges,
     exchange_candidates,
     resolve_exchange,
     tune_exchange,
@@ -657,14 +658,15 @@ def main() -> int:
     exchange = resolve_exchange(args.exchange, world)
     selection = "fixed" if args.exchange != "auto" else "cost model"
     tuned = None
+    chunk_shape = "even"
     if sharded and args.exchange == "auto" and not args.no_tune:
         # time every (exchange, chunks) candidate on this node before the warmup (untimed; the
         # max over ranks decides, so every rank picks the same): the link rate the DESIGN.md §5
         # cost model assumes is not measurable on one GPU
-        (exchange, args.chunks), times = tune_exchange(
+        (exchange, args.chunks, chunk_shape), times = tune_exchange(
             reducer, local_totals, exchange_candidates(None if chunks_auto else args.chunks), rounds=3,
             global_total_weights=global_totals, comm=comm, force_collective=args.force_collective)
-        tuned = {f"{e}/{c}": round(ms, 4) for (e, c), ms in times.items()}
+        tuned = {f"{e}/{c}/{sh}": round(ms, 4) for (e, c, sh), ms in times.items()}
         selection = "tuned"
 
     def step() -> None:
@@ -672,7 +674,8 @@ def main() -> int:
         # rank 0 ends the round on the host: sharded_reduce reads the NaN flags there (the
         # reference's assertions, fed_avg_algorithm.py:35,93,97)
         sharded_reduce(reducer, local_totals, chunks=args.chunks, global_total_weights=global_totals,
-                       force_collective=args.force_collective, comm=comm, exchange=exchange, check_nan=False)
+                       force_collective=args.force_collective, comm=comm, exchange=exchange, check_nan=False,
+                       shape=chunk_shape)
         host_enqueue[0] += time.perf_counter() - h0
         if rank == 0:
             reducer.raise_on_nan()
@@ -727,7 +730,7 @@ def main() -> int:
     if comm is not None and n_waves == 1:
         # native round: one timed launch per round, the first chunk's partial kernel (events
         # around every chunk would put markers into the pipeline they measure)
-        a, b = ctx.tile_range(0, ctx.num_tiles // max(1, min(args.chunks, ctx.num_tiles)))
+        a, b = ctx.tile_range(0, chunk_edges(ctx.num_tiles, args.chunks, chunk_shape)[1])
         rank_bytes = (b - a) * (n_local * in_bytes + 8)
         achieved = rank_bytes / (per_launch_ms * 1e-3) / 1e9 if launches else 0.0
         kernel_desc = f"fedavg_tile_kernel<{kname}, OUT_ACC, 1, true, fma> (partial, first of {args.chunks} chunks)"
@@ -816,7 +819,8 @@ def main() -> int:
                 f"clients sharded over {world} GPUs + chunked RCCL "
                 + ("reduce to rank 0" if exchange == "reduce" else "reduce-scatter, per-rank finalize, gather to rank 0")),
             "exchange": None if not sharded else {
-                "mode": exchange, "chunks": args.chunks, "comm": args.comm, "selection": selection,
+                "mode": exchange, "chunks": args.chunks, "chunk_shape": chunk_shape, "comm": args.comm,
+                "selection": selection,
                 "tuned_ms_per_round": tuned,
                 "partial_only_ms_per_step": None if partial_only_ms is None else round(partial_only_ms, 4),
                 "exposed_exchange_and_finalize_ms": (None if partial_only_ms is None

@@ -27,6 +27,7 @@ ERR_HIP = 5
 ERR_STATE = 6
 ERR_RCCL = 7
 COMM_ID_BYTES = 128
+EXCHANGE_REDUCE, EXCHANGE_SCATTER = 0, 1  # FEDAVG_EXCHANGE_* (fedavg_sharded_round_edges)
 FLAG_ACC_NAN = 0x1
 FLAG_RESULT_NAN = 0x2
 FLAG_CENTRAL_NAN = 0x4
@@ -135,6 +136,8 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_sharded_round": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_sharded_round_scatter": (
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "fedavg_sharded_round_edges": (
+        c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int32), c_int32, c_int32, c_int32, c_void_p]),
 }
 
 _lib: ctypes.CDLL | None = None

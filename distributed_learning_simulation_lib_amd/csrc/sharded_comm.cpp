@@ -184,6 +184,31 @@ ncclResult_t gather_windows(fedavg_comm* c, const char* send, char* recv, size_t
   return res != ncclSuccess ? res : end;
 }
 
+// Tile edges of `chunks` equal ranges of n tiles (empty ranges dropped).
+std::vector<int32_t> even_edges(int32_t n, int32_t chunks) {
+  chunks = std::max(1, std::min(chunks, n));
+  std::vector<int32_t> e{0};
+  for (int32_t k = 0; k < chunks; ++k) {
+    const int32_t te = static_cast<int32_t>((static_cast<int64_t>(n) * (k + 1)) / chunks);
+    if (te > e.back()) e.push_back(te);
+  }
+  return e;
+}
+
+// Caller-given edges: 0 = e[0] < e[1] < ... < e[m-1] = n.
+int32_t check_edges(const int32_t* e, int32_t m, int32_t n) {
+  if (!e || m < 2 || e[0] != 0 || e[m - 1] != n)
+    return fedavg_internal_fail(FEDAVG_ERR_INVALID, "tile edges must run from 0 to the context's tile count");
+  for (int32_t i = 1; i < m; ++i)
+    if (e[i] <= e[i - 1]) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "tile edges must increase");
+  return FEDAVG_OK;
+}
+
+int32_t round_reduce(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                     const std::vector<int32_t>& edges, int32_t root, void* stream);
+int32_t round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                      const std::vector<int32_t>& edges, int32_t root, void* stream);
+
 }  // namespace
 
 extern "C" {
@@ -247,11 +272,42 @@ int32_t fedavg_comm_destroy(fedavg_comm* c) {
 int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
                              int32_t chunks, int32_t root, void* stream) {
   if (!c || !ctx || !partial) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
-  if (root < 0 || root >= c->world) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "bad root");
-  if (c->rank == root && !finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "root needs a finalize plan");
   const int32_t n = fedavg_num_tiles(ctx);
   if (n <= 0) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "context has no tiles");
-  chunks = std::max(1, std::min(chunks, n));
+  return round_reduce(c, ctx, partial, finalize, even_edges(n, chunks), root, stream);
+}
+
+int32_t fedavg_sharded_round_edges(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                                   const int32_t* tile_edges, int32_t num_edges, int32_t exchange, int32_t root,
+                                   void* stream) {
+  if (!c || !ctx || !partial) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
+  const int32_t n = fedavg_num_tiles(ctx);
+  if (n <= 0) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "context has no tiles");
+  if (int32_t st = check_edges(tile_edges, num_edges, n)) return st;
+  std::vector<int32_t> edges(tile_edges, tile_edges + num_edges);
+  if (exchange == FEDAVG_EXCHANGE_REDUCE) return round_reduce(c, ctx, partial, finalize, edges, root, stream);
+  if (exchange == FEDAVG_EXCHANGE_SCATTER) return round_scatter(c, ctx, partial, finalize, edges, root, stream);
+  return fedavg_internal_fail(FEDAVG_ERR_INVALID, "exchange must be FEDAVG_EXCHANGE_REDUCE or _SCATTER");
+}
+
+int32_t fedavg_sharded_round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                                     int32_t chunks, int32_t root, void* stream) {
+  if (!c || !ctx || !partial || !finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
+  const int32_t n = fedavg_num_tiles(ctx);
+  if (n <= 0) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "context has no tiles");
+  return round_scatter(c, ctx, partial, finalize, even_edges(n, chunks), root, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+int32_t round_reduce(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                     const std::vector<int32_t>& edges, int32_t root, void* stream) {
+  if (root < 0 || root >= c->world) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "bad root");
+  if (c->rank == root && !finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "root needs a finalize plan");
+  const int32_t n = edges.back();
+  const int32_t chunks = static_cast<int32_t>(edges.size()) - 1;
   COMM_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (int32_t st = ensure_events(c, chunks)) return st;
@@ -263,10 +319,8 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
     int32_t prof;
     ~Restore() { fedavg_internal_set_prof(ctx, prof); }
   } restore{ctx, prof};
-  int32_t tb = 0;
   for (int32_t k = 0; k < chunks; ++k) {
-    const int32_t te = static_cast<int32_t>((static_cast<int64_t>(n) * (k + 1)) / chunks);
-    if (te <= tb) continue;
+    const int32_t tb = edges[k], te = edges[k + 1];
     fedavg_internal_set_prof(ctx, (k == 0) ? prof : 0);
     // the chunk's event completes with its kernel (no marker packet between chunk kernels)
     hipEvent_t ev = c->chunk_events[k];
@@ -277,7 +331,6 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
     ncclResult_t res = rccl().reduce(acc + a, acc + a, static_cast<size_t>(b - a), ncclFloat64, ncclSum, root,
                                      c->nccl, c->stream);
     if (res != ncclSuccess) return rccl_fail(res, "ncclReduce");
-    tb = te;
   }
   // The compute stream goes on once the last reduce has landed (the reduces run in order); the
   // root then divides every tile in one launch. (Dividing each chunk on the comm stream right
@@ -292,16 +345,14 @@ int32_t fedavg_sharded_round(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* parti
   return FEDAVG_OK;
 }
 
-int32_t fedavg_sharded_round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
-                                     int32_t chunks, int32_t root, void* stream) {
-  if (!c || !ctx || !partial || !finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "null argument");
+int32_t round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                      const std::vector<int32_t>& edges, int32_t root, void* stream) {
+  if (!finalize) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "every rank needs a finalize plan");
   if (root < 0 || root >= c->world) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "bad root");
   const int32_t odt = fedavg_plan_out_dtype(finalize);
   if (odt != FEDAVG_F32 && odt != FEDAVG_F64)
     return fedavg_internal_fail(FEDAVG_ERR_INVALID, "every rank needs a finalize plan (fp32 / fp64 outputs)");
-  const int32_t n = fedavg_num_tiles(ctx);
-  if (n <= 0) return fedavg_internal_fail(FEDAVG_ERR_INVALID, "context has no tiles");
-  chunks = std::max(1, std::min(chunks, n));
+  const int32_t chunks = static_cast<int32_t>(edges.size()) - 1;
   const int64_t G = c->world;
   const size_t ob = (odt == FEDAVG_F32) ? 4 : 8;
   const ncclDataType_t ndt = (odt == FEDAVG_F32) ? ncclFloat32 : ncclFloat64;
@@ -317,16 +368,14 @@ int32_t fedavg_sharded_round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_pla
   };
   std::vector<Piece> pieces;
   int64_t slice_elems = 0, rem_elems = 0;
-  for (int32_t k = 0, tb = 0; k < chunks; ++k) {
-    const int32_t te = static_cast<int32_t>((static_cast<int64_t>(n) * (k + 1)) / chunks);
-    if (te <= tb) continue;
+  for (int32_t k = 0; k < chunks; ++k) {
+    const int32_t tb = edges[k], te = edges[k + 1];
     int64_t a = 0, b = 0;
     if (int32_t st = fedavg_tile_range(ctx, tb, te, &a, &b)) return st;
     Piece p{tb, te, a, (b - a) / G, (b - a) % G, slice_elems, rem_elems};
     slice_elems += p.L;
     rem_elems += p.R;
     pieces.push_back(p);
-    tb = te;
   }
   const int64_t acc_numel = fedavg_acc_numel(ctx);
   if (int32_t st = ensure_scratch(c, s, static_cast<size_t>(slice_elems + rem_elems), ob * static_cast<size_t>(acc_numel)))
@@ -380,4 +429,4 @@ int32_t fedavg_sharded_round_scatter(fedavg_comm* c, fedavg_ctx* ctx, fedavg_pla
   return FEDAVG_OK;
 }
 
-}  // extern "C"
+}  // namespace

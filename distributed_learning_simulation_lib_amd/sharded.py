@@ -50,6 +50,10 @@ from .fedavg import ClientTable, FedAvgContext, OutputTable
 
 
 EXCHANGES = ("auto", "reduce", "scatter")
+# chunk shapes: equal ranges; the last chunk half the others (a short exchange tail when the
+# exchange keeps up with the fold); the first chunk half the others (the exchange starts sooner
+# when it does not)
+CHUNK_SHAPES = ("even", "taper", "ramp")
 
 
 def resolve_exchange(exchange: str, world: int) -> str:
@@ -172,25 +176,33 @@ class HipLocalReducer:
             self.ctx.finalize_range(self.outs, self.out_dtype, tile_begin, tile_end)
 
     def native_round(self, comm: RcclComm, total_weights: Sequence[float], chunks: int, root: int,
-                     exchange: str = "reduce") -> None:
-        """One round through the library's own RCCL pipeline (``fedavg_sharded_round`` or
-        ``fedavg_sharded_round_scatter``): the chunk launches, the exchange and the finalize are
-        enqueued by one native call."""
+                     exchange: str = "reduce", shape: str = "even") -> None:
+        """One round through the library's own RCCL pipeline (``fedavg_sharded_round`` /
+        ``_scatter``, or ``fedavg_sharded_round_edges`` for an uneven chunk ``shape``): the chunk
+        launches, the exchange and the finalize are enqueued by one native call."""
         assert self.use_plan and self.table is not None
         if self._partial_plan is None:
             self._partial_plan = self.ctx.plan_partial(self.table, self.in_dtype, zero_init=not self.prior_waves)
         lib = self.ctx._lib
+        fin = None
         if exchange == "scatter":
             self._plan_finalize([float(w) for w in total_weights])
-            _native.check(lib.fedavg_sharded_round_scatter(comm.handle, self.ctx._h, self._partial_plan._h,
-                                                           self._finalize_plan._h, chunks, root, self.ctx.stream))
-            return
-        fin = None
-        if comm.rank == root:
+            fin = self._finalize_plan._h
+        elif comm.rank == root:
             self.set_accumulated(total_weights)
             fin = self._finalize_plan._h
-        _native.check(lib.fedavg_sharded_round(comm.handle, self.ctx._h, self._partial_plan._h, fin,
-                                               chunks, root, self.ctx.stream))
+        if shape != "even":
+            edges = chunk_edges(self.num_tiles, chunks, shape)
+            arr = (ctypes.c_int32 * len(edges))(*edges)
+            ex = _native.EXCHANGE_SCATTER if exchange == "scatter" else _native.EXCHANGE_REDUCE
+            _native.check(lib.fedavg_sharded_round_edges(comm.handle, self.ctx._h, self._partial_plan._h, fin, arr,
+                                                         len(edges), ex, root, self.ctx.stream))
+        elif exchange == "scatter":
+            _native.check(lib.fedavg_sharded_round_scatter(comm.handle, self.ctx._h, self._partial_plan._h, fin,
+                                                           chunks, root, self.ctx.stream))
+        else:
+            _native.check(lib.fedavg_sharded_round(comm.handle, self.ctx._h, self._partial_plan._h, fin,
+                                                   chunks, root, self.ctx.stream))
 
     # -- scatter exchange pieces (host-driven path) -----------------------------------------
     def result_buffer(self) -> torch.Tensor:
@@ -261,10 +273,29 @@ class RcclComm:
             pass
 
 
-def chunk_bounds(num_tiles: int, chunks: int) -> list[tuple[int, int]]:
+def chunk_edges(num_tiles: int, chunks: int, shape: str = "even") -> list[int]:
+    """Tile edges 0 = e[0] < ... < e[-1] = num_tiles of ``chunks`` ranges of the given shape."""
+    if shape not in CHUNK_SHAPES:
+        raise ValueError(f"shape must be one of {CHUNK_SHAPES}, not {shape!r}")
     chunks = max(1, min(chunks, num_tiles))
-    edges = [round(i * num_tiles / chunks) for i in range(chunks + 1)]
-    return [(edges[i], edges[i + 1]) for i in range(chunks) if edges[i + 1] > edges[i]]
+    if shape == "even" or chunks == 1:
+        weights = [1.0] * chunks
+    else:
+        weights = [2.0] * chunks
+        weights[-1 if shape == "taper" else 0] = 1.0
+    total, acc, edges = sum(weights), 0.0, [0]
+    for w in weights:
+        acc += w
+        e = round(acc / total * num_tiles)
+        if e > edges[-1]:
+            edges.append(e)
+    edges[-1] = num_tiles
+    return edges
+
+
+def chunk_bounds(num_tiles: int, chunks: int, shape: str = "even") -> list[tuple[int, int]]:
+    edges = chunk_edges(num_tiles, chunks, shape)
+    return [(edges[i], edges[i + 1]) for i in range(len(edges) - 1)]
 
 
 def sharded_reduce(
@@ -278,6 +309,7 @@ def sharded_reduce(
     comm: RcclComm | None = None,
     exchange: str = "auto",
     check_nan: bool = True,
+    shape: str = "even",
 ) -> list[float]:
     """One FedAvg reduce over every rank's shard; the result lands in the root's outputs.
 
@@ -289,7 +321,8 @@ def sharded_reduce(
     ``force_collective`` (tests / measurement of the sharded path on one GPU). With ``comm``
     (the library's own RCCL communicator) a HIP reducer runs the whole round in one native call
     (``fedavg_sharded_round[_scatter]``); otherwise the exchange goes through
-    ``torch.distributed``. ``root`` is a rank of ``group``. With ``check_nan`` the root raises
+    ``torch.distributed``. ``shape`` is the chunk shape (``CHUNK_SHAPES``). ``root`` is a rank of
+    ``group``. With ``check_nan`` the root raises
     the reference's NaN assertions (fed_avg_algorithm.py:35,93,97) before returning; under the
     scatter exchange another rank's failed window reaches the root as a result NaN.
     """
@@ -313,26 +346,33 @@ def sharded_reduce(
     mode = resolve_exchange(exchange, world)
     reducer.prefold()
     if comm is not None and hasattr(reducer, "native_round"):
-        reducer.native_round(comm, global_totals, chunks, root, exchange=mode)
-    elif mode == "scatter":
-        _scatter_exchange(reducer, global_totals, chunks, world, rank, root, root_global, group, host_staged)
+        reducer.native_round(comm, global_totals, chunks, root, exchange=mode, shape=shape)
     else:
-        _reduce_exchange(reducer, global_totals, chunks, rank, root, root_global, group, host_staged)
+        bounds = chunk_bounds(reducer.num_tiles, chunks, shape)
+        if mode == "scatter":
+            _scatter_exchange(reducer, global_totals, bounds, world, rank, root, root_global, group, host_staged)
+        else:
+            _reduce_exchange(reducer, global_totals, bounds, rank, root, root_global, group, host_staged)
     if check_nan and rank == root:
         reducer.raise_on_nan()
     return global_totals
 
 
-def exchange_candidates(chunks: int | None = None) -> list[tuple[str, int]]:
-    """(exchange, chunks) pairs ``tune_exchange`` tries: both exchanges at 2 / 4 / 8 chunks, or
-    at the given chunk count only."""
-    return [(ex, c) for ex in ("reduce", "scatter") for c in ((chunks,) if chunks else (2, 4, 8))]
+def exchange_candidates(chunks: int | None = None, shapes: Sequence[str] = CHUNK_SHAPES) -> list[tuple[str, int, str]]:
+    """(exchange, chunks, shape) triples ``tune_exchange`` tries: both exchanges at 2 / 4 / 8
+    chunks (or the given count only), every chunk shape (one shape when there is one chunk)."""
+    out = []
+    for ex in ("reduce", "scatter"):
+        for c in ((chunks,) if chunks else (2, 4, 8)):
+            for sh in (shapes if c > 1 else ("even",)):
+                out.append((ex, c, sh))
+    return out
 
 
 def tune_exchange(
     reducer: LocalReducer,
     local_total_weights: Sequence[float],
-    candidates: Sequence[tuple[str, int]] | None = None,
+    candidates: Sequence[tuple[str, int, str]] | None = None,
     rounds: int = 3,
     root: int = 0,
     group: dist.ProcessGroup | None = None,
@@ -340,8 +380,8 @@ def tune_exchange(
     comm: RcclComm | None = None,
     force_collective: bool = False,
     check_nan: bool = True,
-) -> tuple[tuple[str, int], dict[tuple[str, int], float]]:
-    """Pick the exchange and chunk count by timing the job itself.
+) -> tuple[tuple[str, int, str], dict[tuple[str, int, str], float]]:
+    """Pick the exchange, chunk count and chunk shape by timing the job itself.
 
     The cost model of DESIGN.md §5 rests on a link rate no single-GPU box can measure, so the
     multi-GPU round can instead be tuned on the node it runs on: each candidate runs one
@@ -351,16 +391,18 @@ def tune_exchange(
     with the root reading the NaN flags (``check_nan``): without that host sync, back-to-back
     rounds overlap one round's exchange with the next round's fold, a pipelining no
     round-by-round server gets, and the candidates would be ranked on it. Ties go to the earlier candidate.
-    Returns ``((exchange, chunks), {candidate: ms per round})``. Collective: every rank of
+    Returns ``((exchange, chunks, shape), {candidate: ms per round})``. Collective: every rank of
     ``group`` calls it with the same candidates.
     """
     cands = list(candidates) if candidates is not None else exchange_candidates()
     if not cands:
         raise ValueError("no candidates to tune")
-    for ex, ch in cands:
+    for ex, ch, sh in cands:
         resolve_exchange(ex, 2)
         if ch < 1:
             raise ValueError(f"chunks must be >= 1, not {ch}")
+        if sh not in CHUNK_SHAPES:
+            raise ValueError(f"shape must be one of {CHUNK_SHAPES}, not {sh!r}")
     acc = reducer.accumulator
     on_host = not acc.is_cuda or dist.get_backend(group) == "gloo"
 
@@ -368,10 +410,10 @@ def tune_exchange(
         if acc.is_cuda:
             torch.cuda.synchronize(acc.device)
 
-    times: dict[tuple[str, int], float] = {}
-    for ex, ch in cands:
+    times: dict[tuple[str, int, str], float] = {}
+    for ex, ch, sh in cands:
         kw = dict(chunks=ch, root=root, group=group, global_total_weights=global_total_weights,
-                  force_collective=force_collective, comm=comm, exchange=ex, check_nan=check_nan)
+                  force_collective=force_collective, comm=comm, exchange=ex, check_nan=check_nan, shape=sh)
         sharded_reduce(reducer, local_total_weights, **kw)
         settle()
         dist.barrier(group=group)
@@ -382,14 +424,13 @@ def tune_exchange(
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                           device="cpu" if on_host else acc.device)
         dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
-        times[(ex, ch)] = float(el.item()) / max(1, rounds) * 1e3
+        times[(ex, ch, sh)] = float(el.item()) / max(1, rounds) * 1e3
     best = min(range(len(cands)), key=lambda i: (times[cands[i]], i))
     return cands[best], times
 
 
-def _reduce_exchange(reducer: LocalReducer, global_totals: list[float], chunks: int, rank: int, root: int,
-                     root_global: int, group: dist.ProcessGroup | None, host_staged: bool) -> None:
-    bounds = chunk_bounds(reducer.num_tiles, chunks)
+def _reduce_exchange(reducer: LocalReducer, global_totals: list[float], bounds: list[tuple[int, int]], rank: int,
+                     root: int, root_global: int, group: dist.ProcessGroup | None, host_staged: bool) -> None:
     acc = reducer.accumulator
     # Each chunk's reduce is issued right after its partial kernel, from the compute stream:
     # the process group's RCCL stream waits only for that chunk's kernel (an event on the
@@ -424,10 +465,10 @@ def scatter_windows(a: int, b: int, world: int) -> tuple[int, int]:
     return divmod(b - a, world)
 
 
-def _scatter_exchange(reducer: LocalReducer, global_totals: list[float], chunks: int, world: int, rank: int,
-                      root: int, root_global: int, group: dist.ProcessGroup | None, host_staged: bool) -> None:
+def _scatter_exchange(reducer: LocalReducer, global_totals: list[float], bounds: list[tuple[int, int]], world: int,
+                      rank: int, root: int, root_global: int, group: dist.ProcessGroup | None,
+                      host_staged: bool) -> None:
     """Host-driven form of fedavg_sharded_round_scatter (same windows, same arithmetic)."""
-    bounds = chunk_bounds(reducer.num_tiles, chunks)
     acc = reducer.accumulator
     reducer.set_accumulated(global_totals)  # every rank divides its own windows
     res = reducer.result_buffer()

@@ -402,6 +402,19 @@ int32_t fedavg_sharded_round(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* pa
  */
 int32_t fedavg_sharded_round_scatter(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* partial,
                                      fedavg_plan* finalize, int32_t chunks, int32_t root, void* stream);
+/*
+ * Either round with caller-chosen chunks: tile_edges[0..num_edges) runs from 0 to
+ * fedavg_num_tiles(ctx), strictly increasing; chunk k is tiles [tile_edges[k], tile_edges[k+1]).
+ * Uneven chunks shift the exposed part of the exchange: a short last chunk shortens the tail when
+ * the exchange keeps up with the fold, a short first chunk starts the exchange sooner when it
+ * does not (sharded.tune_exchange times the shapes on the node). exchange: FEDAVG_EXCHANGE_*.
+ * fedavg_sharded_round(..., chunks, ...) is this call with `chunks` equal ranges.
+ */
+#define FEDAVG_EXCHANGE_REDUCE 0
+#define FEDAVG_EXCHANGE_SCATTER 1
+int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
+                                   const int32_t* tile_edges, int32_t num_edges, int32_t exchange, int32_t root,
+                                   void* stream);
 
 #ifdef __cplusplus
 }

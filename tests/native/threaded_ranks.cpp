@@ -6,7 +6,7 @@
 // contiguous blocks, every rank folds its shard into an fp64 partial (fedavg_plan_create_partial),
 // and the round goes through fedavg_sharded_round (reduce to the root) and
 // fedavg_sharded_round_scatter (reduce-scatter + per-rank window finalize + gather) at 1, 3 and 4
-// chunks, fp64 and fp32 outputs, roots 0 and G - 1, two rounds on the same plans. The root's
+// chunks and two uneven chunkings (fedavg_sharded_round_edges), fp64 and fp32 outputs, roots 0 and G - 1, two rounds on the same plans. The root's
 // outputs are compared bit-for-bit with the host composition the fake's sums define: per-rank
 // arrival-order fold (acc = -0.0; acc += double(x) * w), the partials added in rank order, then
 // / W (and the fp32 cast). A NaN in the last rank's shard must fail the root's fedavg_check under
@@ -173,9 +173,14 @@ void rank_main(World* w, int rank) {
     }
   };
 
+  // uneven chunks through fedavg_sharded_round_edges (chunks < 0 below): a short first chunk,
+  // then a long one; a short last chunk
+  const int32_t ntiles = fedavg_num_tiles(ctx);
+  const std::vector<int32_t> edges_a = {0, 1, ntiles / 2, ntiles};
+  const std::vector<int32_t> edges_b = {0, ntiles - 2, ntiles - 1, ntiles};
   int checked = 0;
   for (int scatter = 0; scatter < 2; ++scatter)
-    for (int chunks : {1, 3, 4})
+    for (int chunks : {1, 3, 4, -1, -2})
       for (int f32 = 0; f32 < 2; ++f32)
         for (int round = 0; round < 2; ++round) {
           fedavg_plan* fin = f32 ? fin32 : fin64;
@@ -183,10 +188,17 @@ void rank_main(World* w, int rank) {
           for (int t = 0; t < T; ++t)
             RK_HIP(hipMemsetAsync(outs[t], 0xFF, kNumel[t] * (f32 ? 4 : 8), stream));
           RK_ST(fedavg_reset(ctx, stream));
-          if (scatter)
+          fedavg_plan* fin_rank = (scatter || rank == w->root) ? fin : nullptr;
+          if (chunks < 0) {
+            const auto& e = chunks == -1 ? edges_a : edges_b;
+            RK_ST(fedavg_sharded_round_edges(comm, ctx, partial, fin_rank, e.data(), static_cast<int32_t>(e.size()),
+                                             scatter ? FEDAVG_EXCHANGE_SCATTER : FEDAVG_EXCHANGE_REDUCE, w->root,
+                                             stream));
+          } else if (scatter) {
             RK_ST(fedavg_sharded_round_scatter(comm, ctx, partial, fin, chunks, w->root, stream));
-          else
-            RK_ST(fedavg_sharded_round(comm, ctx, partial, rank == w->root ? fin : nullptr, chunks, w->root, stream));
+          } else {
+            RK_ST(fedavg_sharded_round(comm, ctx, partial, fin_rank, chunks, w->root, stream));
+          }
           RK_ST(fedavg_check(ctx, stream, nullptr));
           if (rank == w->root) {
             check_root(std::string(scatter ? "scatter" : "reduce") + " G=" + std::to_string(G) + " root=" +

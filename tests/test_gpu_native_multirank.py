@@ -41,6 +41,6 @@ def test_native_round_with_threaded_ranks(lib):
     proc = subprocess.run([str(exe)], capture_output=True, text=True, timeout=150, env=env)
     assert proc.returncode == 0, proc.stdout + proc.stderr
     for g in (2, 3, 4):
-        assert f"G={g} root=0: 24 root rounds checked" in proc.stdout, proc.stdout
-        assert f"G={g} root={g - 1}: 24 root rounds checked" in proc.stdout, proc.stdout
+        assert f"G={g} root=0: 40 root rounds checked" in proc.stdout, proc.stdout
+        assert f"G={g} root={g - 1}: 40 root rounds checked" in proc.stdout, proc.stdout
     assert proc.stdout.strip().endswith("PASS")

@@ -34,8 +34,8 @@ def nccl_group(hip_device):
 
 @pytest.mark.parametrize("exchange", ["reduce", "scatter"])
 @pytest.mark.parametrize("native", [False, True])
-@pytest.mark.parametrize("chunks", [1, 3, 8])
-def test_forced_collective_matches_fused(chunks, native, exchange, hip_device, nccl_group):
+@pytest.mark.parametrize("chunks,shape", [(1, "even"), (3, "even"), (8, "even"), (3, "taper"), (4, "ramp")])
+def test_forced_collective_matches_fused(chunks, shape, native, exchange, hip_device, nccl_group):
     rng = np.random.default_rng(chunks)
     layout = ModelLayout(names=("a", "b", "c"), shapes=((70001,), (33, 65), (9000,)))
     g = torch.Generator().manual_seed(chunks)
@@ -57,7 +57,8 @@ def test_forced_collective_matches_fused(chunks, native, exchange, hip_device, n
     for _ in range(2):  # a second round reuses the plans and the communicator's events
         for o in out_b:
             o.fill_(float("nan"))
-        got = sharded_reduce(red, totals, chunks=chunks, force_collective=True, comm=comm, exchange=exchange)
+        got = sharded_reduce(red, totals, chunks=chunks, force_collective=True, comm=comm, exchange=exchange,
+                             shape=shape)
         assert got == totals
         ctx_b.raise_on_nan()
         for a, b in zip(out_a, out_b):
@@ -84,6 +85,16 @@ def test_native_comm_rejects_bad_arguments(hip_device, nccl_group):
     # the scatter round needs a finalize plan on every rank
     assert lib.fedavg_sharded_round_scatter(comm.handle, ctx._h, plan._h, None, 1, 0, None) == _native.ERR_INVALID
     assert lib.fedavg_sharded_round_scatter(comm.handle, ctx._h, plan._h, plan._h, 1, 0, None) == _native.ERR_INVALID
+    # explicit chunk edges must run from 0 to the tile count, strictly increasing
+    import ctypes
+
+    n = ctx.num_tiles
+    for edges in ([0, n + 1], [1, n], [0, 0, n], [0]):
+        arr = (ctypes.c_int32 * len(edges))(*edges)
+        assert lib.fedavg_sharded_round_edges(comm.handle, ctx._h, plan._h, None, arr, len(edges),
+                                              _native.EXCHANGE_REDUCE, 0, None) == _native.ERR_INVALID
+    arr = (ctypes.c_int32 * 2)(0, n)
+    assert lib.fedavg_sharded_round_edges(comm.handle, ctx._h, plan._h, None, arr, 2, 7, 0, None) == _native.ERR_INVALID
     comm.close()
 
 

@@ -217,6 +217,20 @@ def build_cases():
             for _ in range(5)
         ]
 
+    # a state dict of mixed dtypes (fp32 / fp16 / fp64 tensors, an int64 counter like
+    # BatchNorm's num_batches_tracked, a 0-dim fp32 and an empty tensor): the reference converts
+    # each tensor to fp64 on its own (`x.to(f64) * w`, fed_avg_algorithm.py:51-54)
+    mixed = {"w": ((700,), torch.float32), "cnt": ((), torch.int64), "h": ((33,), torch.float16),
+             "s": ((), torch.float32), "e": ((0,), torch.float32), "d": ((5, 2), torch.float64)}
+    c = add("mixed_dtypes", {n: sh for n, (sh, _) in mixed.items()}, torch.float32, 4, _ds_weights(4, 74), 74)
+    c["dtype"] = "mixed"
+    for k, a in enumerate(c["arrivals"]):
+        for i, (n, (sh, dt)) in enumerate(mixed.items()):
+            if dt == torch.int64:
+                a[1][n] = torch.tensor(1000 * (k + 1) + 7, dtype=torch.int64)
+            else:
+                a[1][n] = _gen(sh, dt, 74 * 131 + k * 17 + i)
+
     # ---- errors ----
     c = add("err_nan_input", {"e": (100,)}, torch.float32, 3, [1, 2, 3], 60)
     c["arrivals"][1][1]["e"][17] = float("nan")

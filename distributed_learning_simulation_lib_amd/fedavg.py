@@ -134,6 +134,13 @@ class ClientTable:
         self._ptrs: list[int] = []
         self._weights: list[float] = []
         self._keep: list[torch.Tensor] = []
+        # per entry: element count, element size, device (-1 = host) — checked against the
+        # layout and input format before any launch (an undersized operand would be read out
+        # of bounds by the kernel); -1 / 0 / -2 for absent entries
+        self._numel: list[int] = []
+        self._esize: list[int] = []
+        self._dev: list[int] = []
+        self._validated: set = set()
         self.num_clients = 0
         self._arrays: tuple[np.ndarray, np.ndarray] | None = None
         # per-element weights (fedavg_accumulate_elementwise): pointer + dtype code per entry
@@ -150,13 +157,22 @@ class ClientTable:
             weight_tensors = [None] * self.num_segments
         elif len(weight_tensors) != self.num_segments:
             raise ValueError("weight row does not match the layout")
+        for t in tensors:
+            if t is not None and not t.is_contiguous():
+                raise ValueError("client tensors must be contiguous (the kernel reads them as flat buffers)")
         for t, w, wt in zip(tensors, weights, weight_tensors):
             if t is None:
                 self._ptrs.append(0)
                 self._weights.append(0.0)
                 self._wptrs.append(0)
                 self._wdts.append(_native.F64)
+                self._numel.append(-1)
+                self._esize.append(0)
+                self._dev.append(-2)
             else:
+                self._numel.append(t.numel())
+                self._esize.append(t.element_size())
+                self._dev.append(t.device.index if t.device.type == "cuda" else -1)
                 self._ptrs.append(t.data_ptr())
                 self._weights.append(float(w))
                 self._keep.append(t)
@@ -177,6 +193,25 @@ class ClientTable:
         """Weight pointers and dtype codes, [num_clients][num_segments] (0 = scalar weight)."""
         return (np.asarray(self._wptrs or [0], dtype=np.uint64), np.asarray(self._wdts or [0], dtype=np.int32),
                 np.asarray(self._weights or [0.0], dtype=np.float64))
+
+    def validate(self, numels: Sequence[int], esize: int, device_index: int, key) -> None:
+        """Every present entry holds exactly ``numels[seg]`` elements of ``esize`` bytes on the
+        device (checked once per table and ``key``). Raises ValueError naming the first bad one."""
+        if key in self._validated or self.num_clients == 0:
+            return
+        T = self.num_segments
+        have = np.asarray(self._numel, dtype=np.int64).reshape(self.num_clients, T)
+        es = np.asarray(self._esize, dtype=np.int64).reshape(self.num_clients, T)
+        dev = np.asarray(self._dev, dtype=np.int64).reshape(self.num_clients, T)
+        want = np.broadcast_to(np.asarray(numels, dtype=np.int64), have.shape)
+        present = have >= 0
+        bad = present & ((have != want) | (es != esize) | (dev != device_index))
+        if bad.any():
+            k, t = (int(x) for x in np.argwhere(bad)[0])
+            raise ValueError(
+                f"client {k}, tensor {t}: {have[k, t]} elements of {es[k, t]} bytes on device {dev[k, t]}; "
+                f"the layout and input format need {want[k, t]} of {esize} bytes on device {device_index}")
+        self._validated.add(key)
 
     def arrays(self) -> tuple[np.ndarray, np.ndarray]:
         """The C-ABI arrays (built once per table and cached: a table can be reduced many times)."""
@@ -306,7 +341,15 @@ class FedAvgContext:
     def _check_table(self, table: ClientTable, in_dtype: torch.dtype) -> None:
         if table.num_segments != self.layout.num_segments:
             raise ValueError("client table does not match the layout")
-        dtype_code(in_dtype)
+        code = dtype_code(in_dtype)
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        if code in (_native.QSGD_F32, _native.QSGD_F64):
+            # one uint8 record per tensor (include/fedavg_hip.h record layout)
+            need = [int(self._lib.fedavg_qsgd_record_bytes(n)) for n in self.layout.numels]
+            table.validate(need, 1, dev, ("qsgd", tuple(need), dev))
+        else:
+            esize = torch.empty((), dtype=in_dtype).element_size()
+            table.validate(self.layout.numels, esize, dev, (in_dtype, tuple(self.layout.numels), dev))
 
     # -- hot path --------------------------------------------------------------------
     def accumulate(self, table: ClientTable, in_dtype: torch.dtype) -> None:

@@ -156,3 +156,22 @@ def test_model_cache_copies_to_host_fp64():
     assert mc.parameter["x"].dtype == torch.float64
     assert torch.equal(mc.get_parameter_diff({"x": torch.full((3,), 2.0, dtype=torch.float64)})["x"], torch.ones(3, dtype=torch.float64))
     assert np.all(mc.parameter["x"].numpy() == 1.0)
+
+
+def test_client_table_rejects_operands_the_kernel_would_misread():
+    """A client tensor is read as a flat buffer of the layout's size: non-contiguous views are
+    refused when added, wrong sizes / element sizes / devices before any launch (validate)."""
+    from distributed_learning_simulation_lib_amd.fedavg import ClientTable
+
+    t = ClientTable(2)
+    with pytest.raises(ValueError, match="contiguous"):
+        t.add_client([torch.ones(4, 4).t(), torch.ones(3)], [1.0, 1.0])
+    t.add_client([torch.ones(4, 4), None], [1.0, 1.0])  # an absent tensor is never checked
+    t.add_client([torch.ones(16), torch.ones(3)], [2.0, 2.0])
+    t.validate([16, 3], 4, -1, "ok")  # host tensors, fp32: matches
+    with pytest.raises(ValueError, match="client 1, tensor 1: 3 elements"):
+        t.validate([16, 5], 4, -1, "size")
+    with pytest.raises(ValueError, match="of 4 bytes"):
+        t.validate([16, 3], 2, -1, "dtype")
+    with pytest.raises(ValueError, match="on device -1"):
+        t.validate([16, 3], 4, 0, "device")

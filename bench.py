@@ -516,6 +516,112 @@ def main_qsgd(args: argparse.Namespace) -> int:
     return 0
 
 
+def main_elements(args: argparse.Namespace) -> int:
+    """--shard elements: every rank folds its element range of ALL clients (range_sharded.py):
+    bit-identical to one GPU at any N, the exchange is a gather of the fp32 result. The same
+    256-client job as BASELINE config 3, decomposed by elements instead of by clients."""
+    from distributed_learning_simulation_lib_amd.range_sharded import RangeShard, range_sharded_reduce
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", 0 if args.rehearse else local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        if args.rehearse:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
+    in_dtype, out_dtype = getattr(torch, args.in_dtype), getattr(torch, args.out_dtype)
+    layout = LAYOUTS[args.layout]()
+    P = layout.total_numel
+    n_total = args.total_clients if args.total_clients > 0 else (256 if world > 1 else args.clients_per_gpu)
+    weights = dataset_size_weights(n_total)
+    shard = RangeShard(layout, world, rank, device)
+    T = len(shard.pieces)
+    table = None
+    buckets = None
+    if T:
+        buckets, views = make_clients(shard.sub_layout, 0, n_total, device, in_dtype)
+        table = ClientTable(T)
+        for row, w in zip(views, weights):
+            table.add_client(row, [w] * T)
+    out = torch.empty(P, dtype=out_dtype, device=device) if rank == 0 else None
+
+    def step() -> None:
+        range_sharded_reduce(shard, table, in_dtype, out, out_dtype)
+
+    def sync_all() -> None:
+        torch.cuda.synchronize(device)
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+    if shard.ctx is not None:
+        shard.ctx.prof_collect()
+        shard.ctx.prof_enable(not args.no_kernel_events)
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = (0.0, 0)
+    if shard.ctx is not None:
+        shard.ctx.prof_enable(False)
+        kernel_ms, launches = shard.ctx.prof_collect()
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.rehearse else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return 0
+    in_b, out_b = torch.empty((), dtype=in_dtype).element_size(), torch.empty((), dtype=out_dtype).element_size()
+    step_s = elapsed / args.steps
+    job_bytes = n_total * P * in_b + P * out_b
+    span = shard.hi - shard.lo
+    launch_bytes = n_total * span * in_b + span * out_b
+    per_launch = kernel_ms / max(launches, 1)
+    achieved = launch_bytes / (per_launch * 1e-3) / 1e9 if launches else 0.0
+    short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    kname = {torch.float32: "float", torch.float16: "__half", torch.bfloat16: "bf16_t", torch.float64: "double"}[in_dtype]
+    line = {
+        "metric": METRIC, "value": round(job_bytes / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
+        "config": {
+            "workload": f"fedavg_{args.layout}_{short}_{n_total}_clients_element_ranges_over_{world}_gpus",
+            "total_clients": n_total, "params_per_client": P, "tensors_per_client": layout.num_segments,
+            "in_dtype": args.in_dtype, "accumulate_dtype": "float64", "out_dtype": args.out_dtype,
+            "parallelism": f"element ranges over {world} GPUs (every rank folds its range of all clients, "
+                           "bit-identical to one GPU) + gather of the result to rank 0",
+            "rank0_range": [shard.lo, shard.hi],
+            "baseline_config": "BASELINE.json configs[2] job, decomposed by element range (see DESIGN.md §5d)",
+            **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not an N-GPU measurement"}
+               if args.rehearse else {}),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "traffic_source": None,
+            "kernel": f"fedavg_tile_kernel<{kname}, OUT_F32, 1, true, fma> (rank 0's range)",
+            "bytes_per_timed_launch": launch_bytes, "kernel_ms_per_step": round(kernel_ms / args.steps, 4),
+            "mean_launch_ms": round(per_launch, 4), "launches": launches,
+        },
+        "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
+    del buckets
+    return 0
+
+
 def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -> tuple[float | None, str | None]:
     """HBM bytes per launch of the same kernel and workload from the newest committed
     rocprofv3 PMC summary (scripts/profile.sh -> profiles/<tag>_traffic.json), or None."""
@@ -553,6 +659,9 @@ def main() -> int:
                     help="multi-GPU exchange of the fp64 partials: reduce to rank 0, or reduce-scatter + "
                          "per-rank finalize + gather (auto: the fastest (exchange, chunks) pair timed on the "
                          "node before the warmup; with --no-tune scatter at 2 ranks, reduce above; DESIGN.md §5)")
+    ap.add_argument("--shard", default="clients", choices=["clients", "elements"],
+                    help="N > 1: shard whole clients over the ranks (BASELINE config 3, default) or "
+                         "element ranges of every client (range_sharded.py: bit-identical to one GPU)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N > 1 on a one-GPU box: all ranks on cuda:0 over gloo (host-staged exchange); "
                          "exercises the multi-rank code path, not a measurement")
@@ -577,6 +686,8 @@ def main() -> int:
         return main_personalized(args)
     if args.workload == "qsgd":
         return main_qsgd(args)
+    if args.shard == "elements":
+        return main_elements(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -13,10 +13,6 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "base": {},
-    "buf_nt": {"FEDAVG_RESULT_AUX": 2},
-    "buf_sc01nt": {"FEDAVG_RESULT_AUX": 19},
-    "buf_sc1nt": {"FEDAVG_RESULT_AUX": 18},
-    "buf_sc01": {"FEDAVG_RESULT_AUX": 17},
 }
 VDIR = REPO / "distributed_learning_simulation_lib_amd" / "_lib" / "variants"
 

@@ -63,8 +63,13 @@ from .aggregation_algorithm import (
 )
 
 
+_KERNEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
+
+
 def _is_elementwise(weight: Any, parameter: Any) -> bool:
     """A _get_weight value that is a tensor of the parameter's shape (not a scalar)."""
+    if type(weight) in (int, float):  # the default hook's dataset-size weight: the common case
+        return False
     if isinstance(weight, torch.Tensor) and weight.numel() != 1:
         if isinstance(parameter, torch.Tensor) and tuple(weight.shape) == tuple(parameter.shape):
             return True
@@ -321,18 +326,29 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         tensors: list[torch.Tensor | None] = []
         weights: list[float] = []
         weight_tensors: list[torch.Tensor | None] = []
+        names, shapes, ew = self.__layout.names, self.__layout.shapes, self.__ew
+        dev = self.device
+        dev_idx = dev.index if dev.index is not None else (torch.cuda.current_device() if dev.type == "cuda" else -1)
+        # the common arrival — dense tensors of one kernel dtype, contiguous, already on this
+        # device — is recognised in this one pass and staged without the general path's passes
+        in_place, dtypes = True, set()
         for i in self.__keep:
-            name = self.__layout.names[i]
+            name = names[i]
             if name in row:
                 t, w = row[name]
-                if tuple(t.shape) != self.__layout.shapes[i]:
-                    raise ValueError(f"shape of {name} changed: {tuple(t.shape)} vs {self.__layout.shapes[i]}")
+                if t.shape != shapes[i]:  # torch.Size / tuple compare as tuples
+                    raise ValueError(f"shape of {name} changed: {tuple(t.shape)} vs {shapes[i]}")
                 assert w is not None, "aggregation_weight is None"
                 tensors.append(t)
-                if self.__ew:
+                if in_place:
+                    if isinstance(t, torch.Tensor) and t.get_device() == dev_idx and t.is_contiguous():
+                        dtypes.add(t.dtype)
+                    else:
+                        in_place = False
+                if ew:
                     self.__tot_fp32.setdefault(name, _total_is_fp32(w))
                     if _is_elementwise(w, t):
-                        wt = w.detach().to(device=self.device).contiguous()
+                        wt = w.detach().to(device=dev).contiguous()
                         if wt.dtype not in (torch.float32, torch.float64):
                             wt = wt.to(torch.float64)
                         weight_tensors.append(wt)
@@ -344,23 +360,28 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 tensors.append(None)
                 weights.append(0.0)
                 weight_tensors.append(None)
-        present = [t for t in tensors if t is not None]
-        codecs = {t.codec for t in present if isinstance(t, QuantizedTensor)}
-        if codecs and len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in present) and not self.__ew:
-            # quantised update: the records are the kernel operands (dequantised in the fold)
-            dt = codecs.pop()
-            tensors = self._records_to_device(tensors)
+        if in_place and len(dtypes) == 1 and next(iter(dtypes)) in _KERNEL_DTYPES:
+            dt = next(iter(dtypes))
+        elif in_place and not dtypes:
+            dt = self.__table_dtype or torch.float32
         else:
-            if codecs:  # mixed with dense tensors (e.g. complete()-d keys): dequantise here
-                tensors = [dequantize_tensor(t) if isinstance(t, QuantizedTensor) else t for t in tensors]
-            tensors = self._to_device_row(tensors)
             present = [t for t in tensors if t is not None]
-            if present:
-                unified, dt = unify_dtype(present)
-                it = iter(unified)
-                tensors = [next(it) if t is not None else None for t in tensors]
+            codecs = {t.codec for t in present if isinstance(t, QuantizedTensor)}
+            if codecs and len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in present) and not ew:
+                # quantised update: the records are the kernel operands (dequantised in the fold)
+                dt = codecs.pop()
+                tensors = self._records_to_device(tensors)
             else:
-                dt = self.__table_dtype or torch.float32
+                if codecs:  # mixed with dense tensors (e.g. complete()-d keys): dequantise here
+                    tensors = [dequantize_tensor(t) if isinstance(t, QuantizedTensor) else t for t in tensors]
+                tensors = self._to_device_row(tensors)
+                present = [t for t in tensors if t is not None]
+                if present:
+                    unified, dt = unify_dtype(present)
+                    it = iter(unified)
+                    tensors = [next(it) if t is not None else None for t in tensors]
+                else:
+                    dt = self.__table_dtype or torch.float32
         if self.eager_nan_check:
             self._scan_arrival(tensors, dt, worker_id, delta)
         if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
@@ -387,9 +408,13 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _to_device_row(self, tensors: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
         """One client's tensors in HBM. Host tensors of one kernel dtype go through the pinned
         ingest (one packed DMA per client); anything else moves tensor by tensor."""
-        host = [t for t in tensors if t is not None and t.device.type == "cpu"]
+        host = [t for t in tensors if t is not None and not t.is_cuda]
         if not host:
-            return [None if t is None else to_device_operand(t, self.device) for t in tensors]
+            dev = self.device
+            idx = dev.index if dev.index is not None else torch.cuda.current_device()
+            # device tensors already in place (the common case) are used as they are
+            return [t if t is None or (t.get_device() == idx and t.is_contiguous()) else to_device_operand(t, dev)
+                    for t in tensors]
         dtypes = {t.dtype for t in host}
         if len(dtypes) == 1 and next(iter(dtypes)) in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
             if self.__ingest is None:

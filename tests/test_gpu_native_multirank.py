@@ -43,4 +43,5 @@ def test_native_round_with_threaded_ranks(lib):
     for g in (2, 3, 4):
         assert f"G={g} root=0: 40 root rounds checked" in proc.stdout, proc.stdout
         assert f"G={g} root={g - 1}: 40 root rounds checked" in proc.stdout, proc.stdout
+    assert proc.stdout.count("sweep G=") == 6, proc.stdout  # the randomised layouts
     assert proc.stdout.strip().endswith("PASS")

@@ -157,3 +157,26 @@ def test_range_sharded_gloo_bitwise(world):
 def test_range_sharded_nan_fails_every_rank():
     got = _run(3, nan=(2, 3, 2000))  # segment d, in the last rank's range
     assert all(st == "AssertionError" for st, _ in got.values())
+
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=60, deadline=None)
+@given(sizes=st.lists(st.integers(min_value=1, max_value=30000), min_size=1, max_size=12),
+       world=st.integers(min_value=1, max_value=9))
+def test_pieces_cover_every_element_once(sizes, world):
+    """Any layout, any world: the ranks' pieces tile every tensor exactly once, each piece
+    starts on a multiple of 4096 elements of its tensor (or at its start)."""
+    layout = ModelLayout(names=tuple(f"t{i}" for i in range(len(sizes))), shapes=tuple((n,) for n in sizes))
+    seen = [np.zeros(n, dtype=np.int32) for n in sizes]
+    for rank in range(world):
+        shard = RangeShard(layout, world, rank, None)
+        for p in shard.pieces:
+            assert p.lo % 4096 == 0 or p.lo == 0 or (p.seg, p.lo) == (shard.pieces[0].seg, shard.pieces[0].lo)
+            seen[p.seg][p.lo:p.hi] += 1
+        if shard.pieces:
+            first = shard.pieces[0]
+            assert first.lo % 4096 == 0
+    assert all((s == 1).all() for s in seen)

@@ -29,6 +29,7 @@ from .fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError
 from . import _native
 
 RANGE_ALIGN = 4096  # range boundaries fall on multiples of this many elements (16-B aligned views)
+_FLAG_LOCAL_ERROR = 0x100  # a rank's fold raised (e.g. nothing to aggregate): every rank raises
 
 
 def element_ranges(total: int, world: int, align: int = RANGE_ALIGN) -> list[tuple[int, int]]:
@@ -132,9 +133,12 @@ class RangeShard:
         return self._outs[out_dtype]
 
     def fold(self, table: ClientTable | None, in_dtype: torch.dtype, out_dtype: torch.dtype) -> torch.Tensor:
-        """Fold + divide this rank's range (one fused launch); returns the local result."""
+        """Fold + divide this rank's range (one fused launch); returns the local result. A rank
+        with elements but no clients raises, as the reference does with nothing accumulated."""
         flat, outs = self.local_output(out_dtype)
-        if self.ctx is not None and table is not None:
+        if self.ctx is not None:
+            if table is None or table.num_clients == 0:
+                raise RuntimeError("nothing to aggregate in this rank's range (fed_avg_algorithm.py:88)")
             self.ctx.aggregate(table, in_dtype, outs, out_dtype)
         return flat
 
@@ -170,15 +174,25 @@ def range_sharded_reduce(
     if rank == root:
         if out is None or out.numel() != shard.layout.total_numel or out.dtype != out_dtype or not out.is_contiguous():
             raise ValueError("the root needs a contiguous flat output of the layout's size and dtype")
-    local = shard.fold(table, in_dtype, out_dtype)
-    flags = shard.flags()
+    # a rank whose fold fails still joins the flag reduction below, so no rank waits forever
+    error: Exception | None = None
+    try:
+        local = shard.fold(table, in_dtype, out_dtype)
+        flags = shard.flags()
+    except (RuntimeError, ValueError) as e:
+        error, local, flags = e, torch.empty(0, dtype=out_dtype, device=shard.device), _FLAG_LOCAL_ERROR
     if world > 1:
         host = dist.get_backend(group) == "gloo"
-        f = torch.tensor([flags], dtype=torch.int32, device="cpu" if host or not local.is_cuda else local.device)
+        on_host = host or shard.device is None or torch.device(shard.device).type != "cuda"
+        f = torch.tensor([flags], dtype=torch.int32, device="cpu" if on_host else shard.device)
         dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
         global_flags = int(f.item())
     else:
         global_flags = flags
+    if global_flags & _FLAG_LOCAL_ERROR:
+        if error is not None:
+            raise error
+        raise RuntimeError("another rank's fold of its element range failed")
     if global_flags:
         if flags:
             shard.raise_local([(table, in_dtype)] if table is not None else [])

@@ -97,6 +97,15 @@ class OracleRangeShard(RangeShard):
         raise AssertionError("NaN in this rank's range")
 
 
+class FailingRangeShard(OracleRangeShard):
+    """Rank 1's fold fails (as a rank with elements but no clients does)."""
+
+    def fold(self, table, in_dtype, out_dtype):
+        if self.rank == 1:
+            raise RuntimeError("nothing to aggregate in this rank's range")
+        return super().fold(table, in_dtype, out_dtype)
+
+
 def _clients(n, nan=None):
     g = torch.Generator().manual_seed(3)
     clients = [[torch.randn(s, generator=g) for s in LAYOUT.shapes] for _ in range(n)]
@@ -107,17 +116,21 @@ def _clients(n, nan=None):
     return clients, weights
 
 
-def _worker(rank, world, port, nan, q):
+def _worker(rank, world, port, nan, q, failing=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         clients, weights = _clients(6, nan)
-        shard = OracleRangeShard(LAYOUT, world, rank, None, clients=clients, weights=weights)
+        cls = FailingRangeShard if failing else OracleRangeShard
+        shard = cls(LAYOUT, world, rank, None, clients=clients, weights=weights)
         out = torch.empty(LAYOUT.total_numel, dtype=torch.float64) if rank == 0 else None
         try:
             range_sharded_reduce(shard, None, torch.float32, out, torch.float64)
         except AssertionError:
             q.put((rank, "AssertionError", None))
+            return
+        except RuntimeError:
+            q.put((rank, "RuntimeError", None))
             return
         q.put((rank, "ok", out.numpy() if rank == 0 else None))
     finally:
@@ -130,11 +143,11 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(world, nan=None):
+def _run(world, nan=None, failing=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nan, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nan, q, failing)) for r in range(world)]
     for p in procs:
         p.start()
     got = {r: (st, v) for r, st, v in (q.get(timeout=120) for _ in range(world))}
@@ -152,6 +165,11 @@ def test_range_sharded_gloo_bitwise(world):
                            for s in range(LAYOUT.num_segments)])
     assert got[0][0] == "ok"
     assert np.array_equal(got[0][1].view(np.uint64), want.view(np.uint64))
+
+
+def test_a_failed_fold_fails_every_rank_without_a_hang():
+    got = _run(3, failing=True)
+    assert all(st == "RuntimeError" for st, _ in got.values())
 
 
 def test_range_sharded_nan_fails_every_rank():

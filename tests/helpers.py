@@ -2,6 +2,8 @@
 
 from __future__ import annotations
 
+import tempfile
+
 import numpy as np
 import torch
 
@@ -56,3 +58,8 @@ def config1_update(worker: int, round_idx: int, numel: int = 1_000_000) -> Param
     g = torch.Generator().manual_seed(1234 + worker + 1000 * round_idx)
     weight = int(np.random.default_rng(99).integers(100, 5001, size=16)[worker])
     return ParameterMessage(parameter={"model": torch.randn(numel, generator=g)}, aggregation_weight=weight)
+
+
+def rendezvous_url() -> str:
+    """A fresh file:// rendezvous for a multi-process test group (no TCP port to race for)."""
+    return "file://" + tempfile.mkdtemp(prefix="fedavg_rdzv_") + "/store"

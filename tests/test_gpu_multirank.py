@@ -14,8 +14,6 @@ result equals the oracle's (S0 + S1) / W bit for bit, and the reference's single
 
 from __future__ import annotations
 
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -24,6 +22,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle.fedavg_oracle import fedavg_flat
+from tests.helpers import rendezvous_url
 
 pytestmark = pytest.mark.gpu
 
@@ -39,8 +38,7 @@ def _clients():
 
 
 def _rank_main(rank, world, port, exchange, pass_totals, nan_client, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         from distributed_learning_simulation_lib_amd.fedavg import ClientTable, FedAvgContext, ModelLayout
         from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, sharded_reduce
@@ -80,9 +78,8 @@ def _rank_main(rank, world, port, exchange, pass_totals, nan_client, q):
 
 
 def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    # a file rendezvous: no TCP port to collide with another test\'s store
+    return rendezvous_url()
 
 
 def _run(exchange, pass_totals, nan_client=None, world=2):

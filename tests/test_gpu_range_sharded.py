@@ -6,8 +6,6 @@ range fails every rank (fed_avg_algorithm.py:35,93,97)."""
 
 from __future__ import annotations
 
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -16,6 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle.fedavg_oracle import fedavg_flat
+from tests.helpers import rendezvous_url
 
 pytestmark = pytest.mark.gpu
 
@@ -31,8 +30,7 @@ def _clients():
 
 
 def _rank_main(rank, world, port, nan_at, out_dtype_name, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         from distributed_learning_simulation_lib_amd.fedavg import ClientTable, ModelLayout
         from distributed_learning_simulation_lib_amd.range_sharded import RangeShard, range_sharded_reduce
@@ -65,9 +63,8 @@ def _rank_main(rank, world, port, nan_at, out_dtype_name, q):
 
 
 def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    # a file rendezvous: no TCP port to collide with another test\'s store
+    return rendezvous_url()
 
 
 def _run(world, nan_at=None, out_dtype="float64"):

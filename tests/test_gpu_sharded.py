@@ -3,8 +3,6 @@ through partial -> chunked RCCL reduce -> chunked finalize, against the fused ke
 
 from __future__ import annotations
 
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -17,17 +15,10 @@ from distributed_learning_simulation_lib_amd.sharded import HipLocalReducer, Rcc
 pytestmark = pytest.mark.gpu
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 @pytest.fixture
 def nccl_group(hip_device):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=hip_device)
+    # one rank: an in-process store, no TCP port to race for
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=hip_device)
     yield
     dist.destroy_process_group()
 

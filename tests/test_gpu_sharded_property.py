@@ -7,8 +7,6 @@ the cross-rank reorder at N > 1 is covered by tests/test_sharded_gloo.py."""
 
 from __future__ import annotations
 
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -27,12 +25,8 @@ TORCH_DT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torc
 
 @pytest.fixture(scope="module")
 def native_comm(hip_device):
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=hip_device)
+    # one rank: an in-process store, no TCP port to race for
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=hip_device)
     comm = RcclComm(hip_device)
     yield comm
     torch.cuda.synchronize(hip_device)

@@ -5,8 +5,6 @@ chain, fed_avg_algorithm.py:43-99), and a NaN in one rank's range fails every ra
 
 from __future__ import annotations
 
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -24,6 +22,7 @@ from distributed_learning_simulation_lib_amd.range_sharded import (
     segment_views,
 )
 from oracle.fedavg_oracle import fedavg_flat
+from tests.helpers import rendezvous_url
 
 LAYOUT = ModelLayout(names=("a", "b", "c", "d"), shapes=((5000,), (3, 7), (9000,), (2049,)))
 
@@ -117,8 +116,7 @@ def _clients(n, nan=None):
 
 
 def _worker(rank, world, port, nan, q, failing=False):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         clients, weights = _clients(6, nan)
         cls = FailingRangeShard if failing else OracleRangeShard
@@ -138,9 +136,8 @@ def _worker(rank, world, port, nan, q, failing=False):
 
 
 def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    # a file rendezvous: no TCP port to collide with another test\'s store
+    return rendezvous_url()
 
 
 def _run(world, nan=None, failing=False):

@@ -10,8 +10,6 @@ segments); the GPU parity tests cover the HIP reducer itself.
 
 from __future__ import annotations
 
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -22,6 +20,7 @@ import torch.multiprocessing as mp
 from distributed_learning_simulation_lib_amd.fedavg import ModelLayout
 from distributed_learning_simulation_lib_amd.sharded import chunk_bounds, sharded_reduce
 from oracle.fedavg_oracle import fedavg_flat
+from tests.helpers import rendezvous_url
 
 TILE = 2048
 
@@ -110,8 +109,7 @@ def make_all_clients(n):
 
 
 def _worker(rank, world, port, n_clients, chunks, pass_totals, q, exchange="reduce", subgroup=False, shape="even"):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         group = None
         if subgroup:  # the shard ranks are global ranks 1..world-1; group rank 0 = global rank 1
@@ -137,9 +135,8 @@ def _worker(rank, world, port, n_clients, chunks, pass_totals, q, exchange="redu
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    # a file rendezvous: no TCP port to collide with another test\'s store
+    return rendezvous_url()
 
 
 @pytest.mark.parametrize("exchange", ["reduce", "scatter"])
@@ -183,8 +180,7 @@ def test_single_rank_uses_the_fused_path():
 
 
 def _nan_worker(rank, world, port, exchange, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         clients, weights = make_all_clients(4)
         if rank == world - 1:
@@ -220,8 +216,7 @@ def test_root_raises_on_a_nan_in_another_shard(exchange):
 def _tune_worker(rank, world, port, q):
     from distributed_learning_simulation_lib_amd.sharded import exchange_candidates, tune_exchange
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         clients, weights = make_all_clients(5)
         mine = [i for i in range(5) if i % world == rank]
@@ -325,8 +320,7 @@ class _FakeCommLib:
 
 
 def _comm_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         from distributed_learning_simulation_lib_amd import _native, sharded
 

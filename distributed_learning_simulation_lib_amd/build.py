@@ -21,7 +21,7 @@ LIB_NAME = "libfedavg_hip.so"
 LIB_PATH = LIB_DIR / LIB_NAME
 SOURCES = [CSRC / "fedavg_kernels.hip", CSRC / "personalized_kernels.hip", CSRC / "host_pack.cpp",
            CSRC / "sharded_comm.cpp"]
-HEADERS = [REPO_DIR / "include" / "fedavg_hip.h"]
+HEADERS = [REPO_DIR / "include" / "fedavg_hip.h", CSRC / "exact_div.h"]
 # C++ clients of the ABI alone (no Python, no torch), built next to the library
 EXAMPLES = {"c_abi_round": REPO_DIR / "examples" / "c_abi_round.cpp",
             # test infrastructure: the native multi-rank round with ranks as threads on one GPU

@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "../../include/fedavg_hip.h"
+#include "exact_div.h"
 
 namespace {
 
@@ -725,14 +726,12 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     const double W = to_const<double>(a.tab.wtot)[seg];
     bool bad_res = false;
     double res[AE];
-#pragma unroll
-    for (int i = 0; i < AE; ++i) {
 #if FEDAVG_ABLATE_EPILOGUE  // timing-only build: reciprocal multiply, no NaN checks (wrong results)
-      res[i] = acc[i] * (1.0 / W);
+#pragma unroll
+    for (int i = 0; i < AE; ++i) res[i] = acc[i] * (1.0 / W);
 #else
-      res[i] = acc[i] / W;
+    exact_div_block<AE>(acc, res, W);
 #endif
-    }
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int e = (v * LANES + li) * N;
@@ -1036,11 +1035,9 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
     const double W = to_const<double>(a.tab.wtot)[seg];
     double res[AE];
     bool bad_res = false;
+    exact_div_block<AE>(acc, res, W);
 #pragma unroll
-    for (int j = 0; j < AE; ++j) {
-      res[j] = acc[j] / W;
-      bad_res |= (FULL || e0 + j < count) && (res[j] != res[j]);
-    }
+    for (int j = 0; j < AE; ++j) bad_res |= (FULL || e0 + j < count) && (res[j] != res[j]);
     void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
     if constexpr (OUT == OUT_F32) {
       const gptr<float> op = to_global_mut<float>(out_raw) + td.start + e0;

@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "../../include/fedavg_hip.h"
+#include "exact_div.h"
 
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_fail(int32_t code, const char* msg);
 
@@ -514,13 +515,17 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
   for (int j = 0; j < kJB; ++j) {
     if (j0 + j >= a.M) continue;  // (continue, not break: keeps the loop fully unrolled)
     const double W = wtot[static_cast<int64_t>(j0 + j) * a.T + seg];
-    double r[kVE];
+    double r[kVE], s[kVE];
 #pragma unroll
     for (int v = 0; v < kVE; ++v) {
       bad_acc |= in[v] && acc[v][j] != acc[v][j];
-      acc[v][j] = acc[v][j] / W;
-      bad_res |= in[v] && acc[v][j] != acc[v][j];
-      r[v] = acc[v][j];
+      s[v] = acc[v][j];
+    }
+    exact_div_block<kVE>(s, r, W);
+#pragma unroll
+    for (int v = 0; v < kVE; ++v) {
+      acc[v][j] = r[v];
+      bad_res |= in[v] && r[v] != r[v];
     }
     store_result<FULL>(outs[static_cast<int64_t>(j0 + j) * a.T + seg], start, e, count, a.out_f32, r);
   }

@@ -332,6 +332,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         # the common arrival — dense tensors of one kernel dtype, contiguous, already on this
         # device — is recognised in this one pass and staged without the general path's passes
         in_place, dtypes = True, set()
+        # the client-table row of the common arrival, built in the same pass (pointers, sizes)
+        ptrs: list[int] = []
+        nums: list[int] = []
+        keep: list[torch.Tensor] = []
+        numels = self.__layout.numels
         for i in self.__keep:
             name = names[i]
             if name in row:
@@ -343,6 +348,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 if in_place:
                     if isinstance(t, torch.Tensor) and t.get_device() == dev_idx and t.is_contiguous():
                         dtypes.add(t.dtype)
+                        ptrs.append(t.data_ptr())
+                        nums.append(numels[i])
+                        keep.append(t)
                     else:
                         in_place = False
                 if ew:
@@ -360,8 +368,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 tensors.append(None)
                 weights.append(0.0)
                 weight_tensors.append(None)
+                ptrs.append(0)
+                nums.append(-1)
+        resident = False
         if in_place and len(dtypes) == 1 and next(iter(dtypes)) in _KERNEL_DTYPES:
             dt = next(iter(dtypes))
+            resident = True
         elif in_place and not dtypes:
             dt = self.__table_dtype or torch.float32
         else:
@@ -390,7 +402,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self.__table = ClientTable(len(self.__keep))
             self.__table_dtype = dt
             self.__table_delta = delta
-        self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
+        if resident and not self.__ew:
+            self.__table.add_resident_client(ptrs, weights, nums, dt.itemsize, dev_idx, keep)
+        else:
+            self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
         self.__has_data = True
         if self.__table.num_clients >= self.wave_size:
             self._flush()

@@ -198,6 +198,28 @@ class ClientTable:
         self.num_clients += 1
         self._arrays = None
 
+    def add_resident_client(self, ptrs: list[int], weights: list[float], numels: list[int], esize: int,
+                            device_index: int, keep: list[torch.Tensor]) -> None:
+        """One client row whose present tensors the caller has already checked: contiguous, on
+        ``device_index``, ``esize``-byte elements, ``numels[seg]`` elements each (``ptrs[seg]``
+        == 0 and ``numels[seg]`` == -1 for an absent tensor). The plugin's staging pass proves
+        all of that while it recognises the common arrival, so the row is committed without
+        touching the tensors again; ``validate`` still checks the recorded sizes before a launch."""
+        T = self.num_segments
+        if len(ptrs) != T or len(weights) != T or len(numels) != T:
+            raise ValueError("client row does not match the layout")
+        self._ptrs += ptrs
+        self._weights += weights
+        self._numel += numels
+        self._esize += [esize if n >= 0 else 0 for n in numels]
+        self._dev += [device_index if n >= 0 else -2 for n in numels]
+        self._wptrs += [0] * T
+        self._wdts += [_native.F64] * T
+        self._keep += keep
+        self._validated.clear()
+        self.num_clients += 1
+        self._arrays = None
+
     def elementwise_arrays(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Weight pointers and dtype codes, [num_clients][num_segments] (0 = scalar weight)."""
         return (np.asarray(self._wptrs or [0], dtype=np.uint64), np.asarray(self._wdts or [0], dtype=np.int32),

@@ -133,6 +133,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__host_totals: dict[str, Any] = {}
         # per-element weights: decided by the round's first update
         self.__ew: bool | None = None
+        # no per-tensor hook overridden: a scalar-weighted arrival is staged in one pass
+        # (process_worker_data), with the default hooks' exact effect
+        cls = type(self)
+        self.__default_hooks = all(getattr(cls, h) is getattr(FedAVGAlgorithm, h)
+                                   for h in ("_accumulate_parameter", "_get_weight", "_note_total"))
         self.__tot_fp32: dict[str, bool] = {}
         self.__ew_totals: torch.Tensor | None = None
 
@@ -226,6 +231,22 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 self._stage_client(delta=True, worker_id=worker_id)
                 return True
         if not is_parameter_message(worker_data):
+            return True
+        w = worker_data.aggregation_weight
+        if self.accumulate and self.__default_hooks and isinstance(w, (int, float)):
+            # the default _accumulate_parameter / _get_weight / _note_total for every tensor of
+            # the update (fed_avg_algorithm.py:43-69: the message's weight, the per-name total
+            # += w in arrival order, the payload released), without a hook call per tensor
+            params = worker_data.parameter
+            totals = self.__host_totals
+            for name in params:
+                if name in totals:
+                    totals[name] += w
+                else:
+                    totals[name] = w
+            self.__row = {name: (t, w) for name, t in params.items()}
+            worker_data.parameter = {}
+            self._stage_client(worker_id=worker_id)
             return True
         self.__row = {}
         for name, parameter in worker_data.parameter.items():

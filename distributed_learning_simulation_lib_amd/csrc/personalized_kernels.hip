@@ -68,9 +68,13 @@ int32_t pfail(int32_t code, const std::string& msg) { return fedavg_internal_fai
 #endif
 constexpr int kVE = PERS_VE;           // elements per lane
 constexpr int kChunk = 64 * kVE;       // elements per workgroup
-constexpr int kJB = 16;                // receivers per wave
-constexpr int kMaxWaves = 8;           // waves per workgroup
-constexpr int kGroup = kMaxWaves * kJB;  // receivers per launch (128)
+#ifndef PERS_JB  // receivers per wave (8 or 16): the fp64 accumulators of a lane are kVE x kJB
+#define PERS_JB 16
+#endif
+constexpr int kJB = PERS_JB;           // receivers per wave
+constexpr int kGroup = 128;            // receivers per launch
+constexpr int kMaxWaves = kGroup / kJB;  // waves per workgroup (8, or 16 at 8 receivers per wave)
+static_assert(kJB == 8 || kJB == 16, "receivers per wave");
 #ifndef PERS_U  // 2 keeps every dtype/fold at <= 168 VGPRs = 3 waves per SIMD (measured best)
 #define PERS_U 2
 #endif
@@ -387,9 +391,10 @@ __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, in
   using G = Glds<T>;
   const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
   const int waves = a.waves;
-  // this wave's clients of a stage: c = wave, wave + waves, ... < kSC (every wave the same count
-  // when waves divides kSC; waves >= kSC: waves < kSC issue one, the others none)
-  const int per = (waves >= kSC) ? (wave < kSC ? 1 : 0) : kSC / waves;
+  // this wave's clients of a stage: c = wave, wave + waves, ... < kSC (a wave-uniform count that
+  // may differ between waves, e.g. 2 / 1 / 1 at 3 waves; waves >= kSC: waves < kSC issue one,
+  // the others none) — each wave waits for its own DMAs only, the barrier for the rest
+  const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
   const int nst = a.Npad / kSC;
   auto issue = [&](int st) {
     char* stage = ring + (st % kRS) * (kSC * G::kSlice);

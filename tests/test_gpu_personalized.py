@@ -129,6 +129,15 @@ def test_random_round_matches_oracle(hip_device, weight_kind):
     _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))
 
 
+@pytest.mark.parametrize("receivers", [40, 72, 100, 120])
+def test_int_weights_ring_with_uneven_wave_counts(hip_device, receivers):
+    # integer weights take the LDS-DMA client ring on whole aligned fp32 chunks; 3 / 5 / 7 / 8
+    # waves of 16 receivers split a ring stage of 4 clients unevenly (or not at all) between waves
+    clients, ww = _random_round(receivers, range(receivers), {"a": (1024,), "b": (300,)}, 110 + receivers,
+                                weight_kind="int")
+    _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))
+
+
 def test_two_receiver_groups_carry_the_central_chain(hip_device):
     # 130 receivers > 120 per launch: the second launch continues the centralized chain
     clients, ww = _random_round(130, range(130), {"a": (257,), "b": (3, 5)}, 102)

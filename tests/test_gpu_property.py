@@ -80,7 +80,7 @@ def test_fedavg_random_rounds_are_bit_identical(hip_device, n, sizes, dtype, kin
 
 
 @SETTINGS
-@given(workers=st.integers(2, 20), n_recv=st.integers(1, 20), sizes=st.lists(st.integers(1, 3000), min_size=1, max_size=3),
+@given(workers=st.integers(2, 60), n_recv=st.integers(1, 60), sizes=st.lists(st.integers(1, 3000), min_size=1, max_size=3),
        dtype=st.sampled_from(list(TORCH_DT)), kind=st.sampled_from(["int", "float", "sparse"]),
        seed=st.integers(0, 2**31 - 1), skip=st.integers(-1, 19))
 def test_personalized_random_rounds_are_bit_identical(hip_device, workers, n_recv, sizes, dtype, kind, seed, skip):

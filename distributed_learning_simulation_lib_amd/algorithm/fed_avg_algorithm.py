@@ -42,6 +42,7 @@ from typing import Any
 import numpy as np
 import torch
 
+from .. import _staging
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
 from ..message import (
@@ -64,6 +65,7 @@ from .aggregation_algorithm import (
 
 
 _KERNEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
+_STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # staging_ext.cpp codes
 
 
 def _is_elementwise(weight: Any, parameter: Any) -> bool:
@@ -135,6 +137,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__ew: bool | None = None
         # no per-tensor hook overridden: a scalar-weighted arrival is staged in one pass
         # (process_worker_data), with the default hooks' exact effect
+        self.__staging_maps: tuple | None = None  # (layout, name -> native segment, native shapes)
         cls = type(self)
         self.__default_hooks = all(getattr(cls, h) is getattr(FedAVGAlgorithm, h)
                                    for h in ("_accumulate_parameter", "_get_weight", "_note_total"))
@@ -238,6 +241,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             # the update (fed_avg_algorithm.py:43-69: the message's weight, the per-name total
             # += w in arrival order, the payload released), without a hook call per tensor
             params = worker_data.parameter
+            if self._stage_natively(params, w):
+                worker_data.parameter = {}
+                return True
             totals = self.__host_totals
             for name in params:
                 if name in totals:
@@ -253,6 +259,44 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self._accumulate_parameter(worker_data=worker_data, name=name, parameter=parameter)
         if self.accumulate:
             self._stage_client(worker_id=worker_id)
+        return True
+
+    def _stage_natively(self, params: Any, w: Any) -> bool:
+        """The default hooks' per-tensor walk of a resident update in one native call
+        (csrc/staging_ext.cpp): per-name totals `+= w` in the update's key order, the row's device
+        pointers, the shape / device / contiguity / dtype checks. False (nothing changed) when
+        the extension is absent or the update needs the general path."""
+        ext = _staging.module()
+        if (ext is None or self.__native_layout is None or self.__layout is None or self.__ew
+                or self.eager_nan_check or not isinstance(params, dict)):
+            return False
+        dev = self.device
+        if dev.type != "cuda":
+            return False
+        dev_idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        if self.__staging_maps is None or self.__staging_maps[0] is not self.__layout:
+            index = {n: -1 for n in self.__layout.names}
+            for j, i in enumerate(self.__keep):
+                index[self.__layout.names[i]] = j
+            shapes = [tuple(self.__layout.shapes[i]) for i in self.__keep]
+            self.__staging_maps = (self.__layout, index, shapes)
+        _, index, shapes = self.__staging_maps
+        res = ext.stage_resident(params, index, shapes, dev_idx, self.__host_totals, w)
+        if res is None:
+            return False
+        ptrs, nums, weights, code, keep = res
+        self.__ew = False
+        dt = _STAGING_DTYPES[code]
+        if self.__table is not None and (self.__table_dtype != dt or self.__table_delta):
+            self._flush()
+        if self.__table is None:
+            self.__table = ClientTable(len(self.__keep))
+            self.__table_dtype = dt
+            self.__table_delta = False
+        self.__table.add_resident_client(ptrs, weights, nums, dt.itemsize, dev_idx, keep)
+        self.__has_data = True
+        if self.__table.num_clients >= self.wave_size:
+            self._flush()
         return True
 
     def _restore_on_host(self, worker_id: int, worker_data: Any) -> Any:

@@ -30,6 +30,12 @@ EXAMPLES = {"c_abi_round": REPO_DIR / "examples" / "c_abi_round.cpp",
 # with ncclGather and without it (the grouped send / recv fallback of sharded_comm.cpp)
 FAKE_RCCL_SRC = REPO_DIR / "tests" / "native" / "fake_rccl.cpp"
 FAKE_RCCL = {"libfake_rccl.so": [], "libfake_rccl_nogather.so": ["-DFAKE_RCCL_NO_GATHER"]}
+# host-side staging of plugin updates: a torch C++ extension (CPU code; the C ABI above stays
+# torch-free), built in-tree into _lib/staging/ so it travels with the snapshot
+STAGING_SRC = CSRC / "staging_ext.cpp"
+STAGING_NAME = "fedavg_staging"
+STAGING_DIR = LIB_DIR / "staging"
+STAGING_PATH = STAGING_DIR / f"{STAGING_NAME}.so"
 
 # -ffp-contract=off: the reference rounds the fp64 product and the fp64 sum separately
 # (torch `x.to(f64) * w` then `acc += tmp`); an FMA would change low bits.
@@ -66,6 +72,7 @@ def build(force: bool = False, verbose: bool = False, defines: dict[str, int] | 
     target = out or LIB_PATH
     if out is None and not defines and not force and not needs_build():
         build_examples(verbose=verbose)
+        build_staging(verbose=verbose)
         return LIB_PATH
     target.parent.mkdir(parents=True, exist_ok=True)
     tmp = target.with_suffix(".so.tmp")
@@ -79,7 +86,20 @@ def build(force: bool = False, verbose: bool = False, defines: dict[str, int] | 
     os.replace(tmp, target)
     if out is None:
         build_examples(verbose=verbose)
+        build_staging(verbose=verbose)
     return target
+
+
+def build_staging(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the staging extension (torch.utils.cpp_extension, g++) into _lib/staging/."""
+    if not force and STAGING_PATH.exists() and STAGING_PATH.stat().st_mtime > STAGING_SRC.stat().st_mtime:
+        return STAGING_PATH
+    from torch.utils import cpp_extension
+
+    STAGING_DIR.mkdir(parents=True, exist_ok=True)
+    cpp_extension.load(name=STAGING_NAME, sources=[str(STAGING_SRC)], build_directory=str(STAGING_DIR),
+                       extra_cflags=["-O3"], verbose=verbose)
+    return STAGING_PATH
 
 
 def _run(cmd: list[str], what: str, verbose: bool) -> None:

@@ -1,0 +1,114 @@
+// staging_ext.cpp — host-side staging of one client update for the plugin path (a torch C++
+// extension, CPU code only; the HIP library's C ABI stays torch-free).
+//
+// FedAVGAlgorithm.process_worker_data (fed_avg_algorithm.py:20-64) walks the update's tensors
+// once per arrival: per tensor the default hooks take the message's weight (:66-69), add it to
+// the per-name total in arrival order (:59-62) and release the payload (:64); the GPU fold needs
+// each tensor's device pointer. In Python that walk costs ~0.9 us per tensor (attribute calls on
+// torch tensors); here it is ~50 ns. stage_resident() either stages the whole update or changes
+// nothing and returns None, so the caller can take its general path (host tensors, mixed dtypes,
+// quantised records, a changed shape, a name the layout does not know, ...).
+#include <torch/extension.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace {
+
+// 0 fp32, 1 fp16, 2 bf16, 3 fp64 (the kernel input dtypes), -1 other
+int dtype_code(c10::ScalarType st) {
+  switch (st) {
+    case c10::ScalarType::Float: return 0;
+    case c10::ScalarType::Half: return 1;
+    case c10::ScalarType::BFloat16: return 2;
+    case c10::ScalarType::Double: return 3;
+    default: return -1;
+  }
+}
+
+bool same_shape(const at::Tensor& t, PyObject* shape) {
+  if (!PyTuple_Check(shape)) return false;
+  const Py_ssize_t nd = PyTuple_GET_SIZE(shape);
+  const auto sizes = t.sizes();
+  if (static_cast<Py_ssize_t>(sizes.size()) != nd) return false;
+  for (Py_ssize_t d = 0; d < nd; ++d) {
+    const long long v = PyLong_AsLongLong(PyTuple_GET_ITEM(shape, d));
+    if (v != sizes[d]) return false;
+  }
+  return true;
+}
+
+// stage_resident(params, index, shapes, device_index, totals, weight)
+//   params: dict name -> tensor (the update, in arrival order of its keys)
+//   index:  dict name -> native segment (-1: a zero-element tensor of the layout)
+//   shapes: list of the native segments' shapes (tuples)
+//   totals: dict name -> running total (updated in place, :59-62), weight: int / float
+// Returns (ptrs, numels, weights, dtype_code, keep) or None (nothing changed).
+py::object stage_resident(py::dict params, py::dict index, py::list shapes, int64_t device_index, py::dict totals,
+                          py::object weight) {
+  const Py_ssize_t T = PyList_GET_SIZE(shapes.ptr());
+  const double w = PyFloat_AsDouble(weight.ptr());
+  if (PyErr_Occurred()) {
+    PyErr_Clear();
+    return py::none();
+  }
+  std::vector<int64_t> seg_of;
+  seg_of.reserve(PyDict_Size(params.ptr()));
+  std::vector<int64_t> ptrs(T, 0), numels(T, -1);
+  std::vector<PyObject*> held(T, nullptr);
+  int code = -2;  // no present tensor yet
+  PyObject *key, *value;
+  Py_ssize_t pos = 0;
+  // pass 1: checks only (nothing is changed unless the whole update qualifies)
+  while (PyDict_Next(params.ptr(), &pos, &key, &value)) {
+    PyObject* seg_obj = PyDict_GetItem(index.ptr(), key);  // borrowed
+    if (seg_obj == nullptr) return py::none();              // a name the layout does not know
+    const long long seg = PyLong_AsLongLong(seg_obj);
+    seg_of.push_back(seg);
+    if (!THPVariable_Check(value)) return py::none();
+    const at::Tensor& t = THPVariable_Unpack(value);
+    if (seg < 0) {  // a zero-element tensor of the layout: no segment, only its total
+      if (t.numel() != 0) return py::none();
+      continue;
+    }
+    if (seg >= T || held[seg] != nullptr) return py::none();
+    if (!t.is_cuda() || t.get_device() != device_index || !t.is_contiguous()) return py::none();
+    const int c = dtype_code(t.scalar_type());
+    if (c < 0 || (code != -2 && c != code)) return py::none();
+    code = c;
+    if (!same_shape(t, PyList_GET_ITEM(shapes.ptr(), seg))) return py::none();
+    ptrs[seg] = reinterpret_cast<int64_t>(t.data_ptr());
+    numels[seg] = t.numel();
+    held[seg] = value;
+  }
+  if (code < 0) return py::none();
+  // pass 2: the default hooks' bookkeeping, in the update's key order
+  pos = 0;
+  while (PyDict_Next(params.ptr(), &pos, &key, &value)) {
+    PyObject* cur = PyDict_GetItem(totals.ptr(), key);  // borrowed
+    if (cur == nullptr) {
+      if (PyDict_SetItem(totals.ptr(), key, weight.ptr()) != 0) throw py::error_already_set();
+    } else {
+      PyObject* sum = PyNumber_InPlaceAdd(cur, weight.ptr());  // `total += weight`
+      if (sum == nullptr) throw py::error_already_set();
+      const int rc = PyDict_SetItem(totals.ptr(), key, sum);
+      Py_DECREF(sum);
+      if (rc != 0) throw py::error_already_set();
+    }
+  }
+  py::list out_ptrs(T), out_numels(T), out_weights(T), keep;
+  for (Py_ssize_t s = 0; s < T; ++s) {
+    out_ptrs[s] = py::int_(ptrs[s]);
+    out_numels[s] = py::int_(numels[s]);
+    out_weights[s] = py::float_(held[s] ? w : 0.0);
+    if (held[s]) keep.append(py::reinterpret_borrow<py::object>(held[s]));
+  }
+  return py::make_tuple(out_ptrs, out_numels, out_weights, code, keep);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "host-side staging of plugin updates (see staging_ext.cpp)";
+  m.def("stage_resident", &stage_resident);
+}

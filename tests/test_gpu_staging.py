@@ -1,0 +1,60 @@
+"""The native staging of plugin updates (csrc/staging_ext.cpp) against the oracle, on the MI355X.
+
+Device-resident updates with the default hooks go through one native call per update; anything
+it does not take (a second dtype in the update, a host tensor, a changed shape, an unknown name)
+falls back to the Python staging with nothing changed. Both must give the reference's bits.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMessage, _staging
+from oracle.fedavg_oracle import OracleFedAvg, OracleMessage
+from tests.golden_io import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {"conv": (8, 3, 3, 3), "empty": (0,), "fc": (10, 33), "bias": (10,), "scalar": ()}
+
+
+def test_extension_is_built_and_loaded():
+    assert _staging.module() is not None, "run __graft_entry__.build(): _lib/staging/fedavg_staging.so is missing"
+
+
+@pytest.mark.parametrize("wave", [1, 3, 64])
+def test_native_and_fallback_arrivals_bit_identical(hip_device, wave):
+    g = torch.Generator().manual_seed(5)
+    rng = np.random.default_rng(5)
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=wave)
+    oracle = OracleFedAvg()
+    for k in range(9):
+        p = {n: torch.randn(s, generator=g) for n, s in SHAPES.items()}
+        dev = {n: t.to(hip_device) for n, t in p.items()}
+        if k == 3:  # a second dtype in one update: the Python path unifies it
+            dev["fc"] = dev["fc"].double()
+            p["fc"] = p["fc"].double()
+        if k == 5:  # a host tensor: the pinned ingest path
+            dev["bias"] = p["bias"]
+        if k == 6:  # a non-contiguous view: the general path makes it contiguous
+            dev["fc"] = dev["fc"].t().contiguous().t()
+        w = int(rng.integers(100, 5000)) if k % 2 else float(rng.uniform(0.5, 9.0))
+        algo.process_worker_data(k, ParameterMessage(parameter=dev, aggregation_weight=w))
+        oracle.process_worker_data(k, OracleMessage(parameter={n: t.numpy() for n, t in p.items()},
+                                                    aggregation_weight=w))
+    got = algo.aggregate_worker_data().parameter
+    want = oracle.aggregate_worker_data().parameter
+    assert list(got) == list(want)
+    for n, v in want.items():
+        assert bits_equal(got[n].cpu().numpy(), v), n
+
+
+def test_changed_shape_still_raises(hip_device):
+    algo = FedAVGAlgorithm(device=hip_device)
+    algo.process_worker_data(0, ParameterMessage(parameter={"a": torch.ones(4, device=hip_device)},
+                                                 aggregation_weight=1.0))
+    with pytest.raises(ValueError, match="shape of a changed"):
+        algo.process_worker_data(1, ParameterMessage(parameter={"a": torch.ones(5, device=hip_device)},
+                                                     aggregation_weight=1.0))

@@ -24,7 +24,7 @@ from typing import Any
 import numpy as np
 import torch
 
-from .. import _native
+from .. import _native, _staging
 from ..fedavg import ModelLayout, NaNAggregationError
 from ..ingest import HostIngest
 from ..message import Message, ModelParameter, MultipleWorkerMessage, ParameterMessage, is_parameter_message, wire_class
@@ -55,6 +55,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         self.__layout: ModelLayout | None = None
         self.__ctx: PersonalizedContext | None = None
         self.__ingest: HostIngest | None = None
+        self.__stage_maps: tuple | None = None  # (layout, name -> position, shapes) for staging_ext
 
     @property
     def device(self) -> torch.device:
@@ -77,6 +78,10 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         assert is_parameter_message(worker_data)
         if self.__layout is None:
             self.__layout = ModelLayout.from_parameters(worker_data.parameter)
+        row_native = self._resident_row(worker_data.parameter)
+        if row_native is not None:
+            self.__arrivals.append((worker_id, worker_data, row_native))
+            return True
         unknown = [k for k in worker_data.parameter if k not in self.__layout.names]
         if unknown:
             raise NotImplementedError(
@@ -91,6 +96,24 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             row.append(t)
         self.__arrivals.append((worker_id, worker_data, self._to_device_row(row)))
         return True
+
+    def _resident_row(self, params: Any) -> list[torch.Tensor | None] | None:
+        """An update already in HBM (contiguous, one kernel dtype, the layout's names and shapes)
+        in layout order, checked in one native call (csrc/staging_ext.cpp); None: the general
+        path below (which also raises the errors)."""
+        ext = _staging.module()
+        dev = self.device
+        if ext is None or dev.type != "cuda" or not isinstance(params, dict):
+            return None
+        layout = self.__layout
+        assert layout is not None
+        if self.__stage_maps is None or self.__stage_maps[0] is not layout:
+            self.__stage_maps = (layout, {n: i for i, n in enumerate(layout.names)},
+                                 [tuple(sh) for sh in layout.shapes])
+        _, index, shapes = self.__stage_maps
+        res = ext.resident_row(params, index, shapes,
+                               dev.index if dev.index is not None else torch.cuda.current_device())
+        return None if res is None else res[0]
 
     def _to_device_row(self, row: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
         assert self.__layout is not None
@@ -159,11 +182,19 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
                     self.__ctx.close()
                 self.__ctx = PersonalizedContext(native, self.device)
             res_dtype = self.result_dtype if self.result_dtype in (torch.float32, torch.float64) else torch.float64
-            bufs = [torch.empty(native.padded_offsets(8)[1], dtype=res_dtype, device=self.device) for _ in receivers]
-            offs, _ = native.padded_offsets(8)
-            outs = [[b[o : o + n] for o, n in zip(offs, native.numels)] for b in bufs]
-            cbuf = torch.empty(native.padded_offsets(8)[1], dtype=torch.float64, device=self.device)
-            couts = [cbuf[o : o + n] for o, n in zip(offs, native.numels)]
+            offs, padded = native.padded_offsets(8)
+            bufs = [torch.empty(padded, dtype=res_dtype, device=self.device) for _ in receivers]
+            cbuf = torch.empty(padded, dtype=torch.float64, device=self.device)
+            # M x T result tensors, already in their shapes (one native call per receiver when the
+            # staging extension is built: ~4k views per 64-receiver ResNet-18 round)
+            ext = _staging.module()
+            if ext is not None:
+                shapes = [tuple(sh) for sh in native.shapes]
+                outs = [ext.views(b, offs, shapes) for b in bufs]
+                couts = ext.views(cbuf, offs, shapes)
+            else:
+                outs = [[b[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, native.shapes)] for b in bufs]
+                couts = [cbuf[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, native.shapes)]
             try:
                 self.__ctx.aggregate(rows, dt, ids, weights, receivers, outs, res_dtype, couts, torch.float64)
             except _native.NativeError as e:
@@ -175,11 +206,10 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             flags = self.__ctx.check()
             if flags:
                 self._raise_nan(flags, rows, dt, native, outs, receivers)
+            kept_names = [layout.names[i] for i in keep]
             for r, j in enumerate(receivers):
-                for s, i in enumerate(keep):
-                    out[j][layout.names[i]] = outs[r][s].view(layout.shapes[i])
-            for s, i in enumerate(keep):
-                central[layout.names[i]] = couts[s].view(layout.shapes[i])
+                out[j].update(zip(kept_names, outs[r]))
+            central.update(zip(kept_names, couts))
         for i, name in enumerate(layout.names):
             if i not in keep:
                 for j in receivers:

@@ -16,10 +16,12 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from . import _native
+from . import _native, _staging
 from .fedavg import ModelLayout, dtype_code, out_code
 
 _PTR = ctypes.POINTER(ctypes.c_void_p)
+# dtype codes of csrc/staging_ext.cpp (the kernel input / output dtypes)
+_STAGING_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3}
 _DBL = ctypes.POINTER(ctypes.c_double)
 _I64 = ctypes.POINTER(ctypes.c_int64)
 
@@ -90,10 +92,23 @@ class PersonalizedContext:
         T = self.layout.num_segments
         numels = self.layout.numels
         ptrs = np.zeros(len(clients) * T, dtype=np.uint64)
-        keep: list[torch.Tensor] = []
+        keep: list = []
+        # the checks + pointer pass of a row in one native call (csrc/staging_ext.cpp) when built;
+        # a row it refuses goes through the loop below, which names the offending tensor
+        ext = _staging.module() if self.device.type == "cuda" else None
+        dev_idx = -1
+        if ext is not None:
+            dev_idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        in_code, out_code_, c_code = (_STAGING_CODES.get(in_dtype, -9), _STAGING_CODES.get(out_dtype, -9),
+                                      _STAGING_CODES.get(central_dtype, -9))
         for k, row in enumerate(clients):
             if len(row) != T:
                 raise ValueError("client row does not match the layout")
+            got = ext.row_pointers(list(row), numels, dev_idx, in_code) if ext is not None else None
+            if got is not None:
+                ptrs[k * T : (k + 1) * T] = got
+                keep.append(row)
+                continue
             for t, x in enumerate(row):
                 if x is None:
                     continue
@@ -103,6 +118,11 @@ class PersonalizedContext:
                 keep.append(x)
         optrs = np.zeros(len(outs) * T, dtype=np.uint64)
         for j, row in enumerate(outs):
+            got = ext.row_pointers(list(row), numels, dev_idx, out_code_) if ext is not None and len(row) == T else None
+            if got is not None:
+                optrs[j * T : (j + 1) * T] = got
+                keep.append(row)
+                continue
             for t, o in enumerate(row):
                 if o.device != self.device or o.dtype != out_dtype or o.numel() != numels[t] or not o.is_contiguous():
                     raise ValueError("output tensors must be contiguous, on the device, of the output dtype and size")
@@ -111,11 +131,16 @@ class PersonalizedContext:
         cptrs = None
         if central is not None:
             cptrs = np.zeros(T, dtype=np.uint64)
-            for t, o in enumerate(central):
+            got = ext.row_pointers(list(central), numels, dev_idx, c_code) if ext is not None and len(central) == T \
+                else None
+            for t, o in enumerate(central if got is None else ()):
                 if o.device != self.device or o.dtype != central_dtype or o.numel() != numels[t] or not o.is_contiguous():
                     raise ValueError("centralized outputs must be contiguous, on the device, of the dtype and size")
                 cptrs[t] = o.data_ptr()
                 keep.append(o)
+            if got is not None:
+                cptrs[:] = got
+                keep.append(central)
         return PersonalizedTables(len(clients), len(outs), in_dtype, out_dtype, central_dtype, ptrs, optrs, cptrs,
                                   tuple(keep))
 

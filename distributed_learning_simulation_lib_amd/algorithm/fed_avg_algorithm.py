@@ -220,6 +220,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             assert len(worker_data.delta_parameter) == len(self._old_parameter)
             if self.__layout is None:
                 self._set_layout(self._old_parameter)
+            w = worker_data.aggregation_weight
+            if self.__default_hooks and isinstance(w, (int, float)) and \
+                    self._stage_natively(worker_data.delta_parameter, w, delta=True):
+                worker_data.delta_parameter = {}
+                return True
             row = {}
             for name, delta in worker_data.delta_parameter.items():
                 row[name] = (delta, self._get_weight(worker_data=worker_data, name=name, parameter=delta))
@@ -261,11 +266,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self._stage_client(worker_id=worker_id)
         return True
 
-    def _stage_natively(self, params: Any, w: Any) -> bool:
+    def _stage_natively(self, params: Any, w: Any, delta: bool = False) -> bool:
         """The default hooks' per-tensor walk of a resident update in one native call
         (csrc/staging_ext.cpp): per-name totals `+= w` in the update's key order, the row's device
-        pointers, the shape / device / contiguity / dtype checks. False (nothing changed) when
-        the extension is absent or the update needs the general path."""
+        pointers, the shape / device / contiguity / dtype checks. ``delta``: the tensors are a
+        DeltaParameterMessage's deltas, folded with restore() fused (x = old + delta). False
+        (nothing changed) when the extension is absent or the update needs the general path."""
         ext = _staging.module()
         if (ext is None or self.__native_layout is None or self.__layout is None or self.__ew
                 or self.eager_nan_check or not isinstance(params, dict)):
@@ -287,12 +293,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         ptrs, nums, weights, code, keep = res
         self.__ew = False
         dt = _STAGING_DTYPES[code]
-        if self.__table is not None and (self.__table_dtype != dt or self.__table_delta):
+        if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
             self._flush()
         if self.__table is None:
             self.__table = ClientTable(len(self.__keep))
             self.__table_dtype = dt
-            self.__table_delta = False
+            self.__table_delta = delta
         self.__table.add_resident_client(ptrs, weights, nums, dt.itemsize, dev_idx, keep)
         self.__has_data = True
         if self.__table.num_clients >= self.wave_size:

@@ -58,3 +58,27 @@ def test_changed_shape_still_raises(hip_device):
     with pytest.raises(ValueError, match="shape of a changed"):
         algo.process_worker_data(1, ParameterMessage(parameter={"a": torch.ones(5, device=hip_device)},
                                                      aggregation_weight=1.0))
+
+
+def _delta_round(hip_device):
+    from distributed_learning_simulation_lib_amd.message import DeltaParameterMessage
+
+    g = torch.Generator().manual_seed(9)
+    old = {n: torch.randn(s, generator=g, dtype=torch.float64) for n, s in SHAPES.items()}
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=3)
+    algo.set_old_parameter(old)
+    for k in range(7):
+        d = {n: torch.randn(s, generator=g).to(hip_device) for n, s in SHAPES.items()}
+        algo.process_worker_data(k, DeltaParameterMessage(delta_parameter=d, aggregation_weight=100 + 17 * k))
+    return {n: t.cpu() for n, t in algo.aggregate_worker_data().parameter.items()}
+
+
+def test_native_delta_staging_matches_python_staging(hip_device, monkeypatch):
+    # fused restore (x = old + delta in the fold) through the native staging and through the Python
+    # staging (pinned to the reference by the golden delta cases): the same bits
+    native = _delta_round(hip_device)
+    monkeypatch.setattr(_staging, "module", lambda: None)
+    python = _delta_round(hip_device)
+    assert list(native) == list(python)
+    for n in native:
+        assert bits_equal(native[n].numpy(), python[n].numpy()), n

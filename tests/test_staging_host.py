@@ -1,0 +1,43 @@
+"""Host logic of the staging extension (csrc/staging_ext.cpp) on CPU tensors: what it refuses
+(everything that is not resident on the GPU goes back to the Python staging unchanged), the
+views it makes, and that a refusal leaves the per-name totals untouched."""
+
+from __future__ import annotations
+
+import pytest
+import torch
+
+from distributed_learning_simulation_lib_amd import _staging
+
+ext = _staging.module()
+pytestmark = pytest.mark.skipif(ext is None, reason="staging extension not built")
+
+
+def test_host_tensors_are_refused_and_totals_untouched():
+    params = {"a": torch.ones(3), "b": torch.ones(2, 2)}
+    totals = {"a": 5.0}
+    res = ext.stage_resident(params, {"a": 0, "b": 1}, [(3,), (2, 2)], 0, totals, 2.0)
+    assert res is None
+    assert totals == {"a": 5.0}
+    assert ext.resident_row(params, {"a": 0, "b": 1}, [(3,), (2, 2)], 0) is None
+    assert ext.row_pointers([torch.ones(3), None], [3, 4], 0, 0) is None
+
+
+def test_unknown_names_and_non_tensors_are_refused():
+    assert ext.stage_resident({"z": torch.ones(1)}, {"a": 0}, [(1,)], 0, {}, 1.0) is None
+    assert ext.stage_resident({"a": [1.0]}, {"a": 0}, [(1,)], 0, {}, 1.0) is None
+    assert ext.stage_resident({"a": torch.ones(1)}, {"a": 0}, [(1,)], 0, {}, object()) is None
+
+
+def test_views_of_a_flat_buffer():
+    flat = torch.arange(40, dtype=torch.float64)
+    vs = ext.views(flat, [0, 8, 24, 39], [(2, 4), (4, 4), (), (1,)])
+    assert [tuple(v.shape) for v in vs] == [(2, 4), (4, 4), (), (1,)]
+    assert torch.equal(vs[0], flat[:8].view(2, 4))
+    assert torch.equal(vs[1], flat[8:24].view(4, 4))
+    assert float(vs[2]) == 24.0 and float(vs[3][0]) == 39.0
+    assert all(v.is_contiguous() for v in vs)
+    vs[1][0, 0] = -1.0  # views, not copies
+    assert flat[8] == -1.0
+    with pytest.raises(IndexError):
+        ext.views(flat, [38], [(4,)])  # outside the buffer

@@ -269,7 +269,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _stage_natively(self, params: Any, w: Any, delta: bool = False) -> bool:
         """The default hooks' per-tensor walk of a resident update in one native call
         (csrc/staging_ext.cpp): per-name totals `+= w` in the update's key order, the row's device
-        pointers, the shape / device / contiguity / dtype checks. ``delta``: the tensors are a
+        pointers, the shape / device / contiguity / dtype checks; contiguous host updates of one
+        dtype are packed and moved by the pinned ingest from the pointers. ``delta``: the tensors are a
         DeltaParameterMessage's deltas, folded with restore() fused (x = old + delta). False
         (nothing changed) when the extension is absent or the update needs the general path."""
         ext = _staging.module()
@@ -287,12 +288,21 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             shapes = [tuple(self.__layout.shapes[i]) for i in self.__keep]
             self.__staging_maps = (self.__layout, index, shapes)
         _, index, shapes = self.__staging_maps
-        res = ext.stage_resident(params, index, shapes, dev_idx, self.__host_totals, w)
+        first = next(iter(params.values()), None)
+        host = isinstance(first, torch.Tensor) and first.device.type == "cpu"
+        res = ext.stage_resident(params, index, shapes, -1 if host else dev_idx, self.__host_totals, w)
         if res is None:
             return False
         ptrs, nums, weights, code, keep = res
         self.__ew = False
         dt = _STAGING_DTYPES[code]
+        if host:
+            # host update: one packed DMA per client through the pinned ingest (ingest.py), the
+            # row's device pointers computed from the bucket's segment offsets
+            if self.__ingest is None:
+                self.__ingest = HostIngest(self.device)
+            bucket, ptrs = self.__ingest.to_device_pointers(self.__native_layout, ptrs, nums, dt)
+            keep = [bucket]
         if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
             self._flush()
         if self.__table is None:

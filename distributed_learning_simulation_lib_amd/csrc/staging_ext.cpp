@@ -46,6 +46,8 @@ bool same_shape(const at::Tensor& t, PyObject* shape) {
 //   index:  dict name -> native segment (-1: a zero-element tensor of the layout)
 //   shapes: list of the native segments' shapes (tuples)
 //   totals: dict name -> running total (updated in place, :59-62), weight: int / float
+//   device_index: the GPU the tensors must already be on, or -1: host tensors (the pinned
+//   ingest then packs them from the returned pointers)
 // Returns (ptrs, numels, weights, dtype_code, keep) or None (nothing changed).
 py::object stage_resident(py::dict params, py::dict index, py::list shapes, int64_t device_index, py::dict totals,
                           py::object weight) {
@@ -72,7 +74,8 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
       continue;
     }
     if (seg >= T || held[seg] != nullptr) return py::none();
-    if (!t.is_cuda() || t.get_device() != device_index || !t.is_contiguous()) return py::none();
+    if (!t.is_contiguous()) return py::none();
+    if (device_index >= 0 ? (!t.is_cuda() || t.get_device() != device_index) : !t.is_cpu()) return py::none();
     const int c = dtype_code(t.scalar_type());
     if (c < 0 || (code != -2 && c != code)) return py::none();
     code = c;

@@ -70,3 +70,28 @@ class HostIngest:
         self._events[key][i] = ev
         self.bytes_moved += padded * elem
         return [None if t is None else bucket[o : o + n] for t, o, n in zip(tensors, offs, layout.numels)]
+
+    def to_device_pointers(
+        self, layout: ModelLayout, ptrs: Sequence[int], numels: Sequence[int], dtype: torch.dtype
+    ) -> tuple[torch.Tensor, list[int]]:
+        """The same transfer for a row the caller has already checked (contiguous host tensors of
+        ``dtype``: their data pointers, ``numels`` = -1 where absent, layout order). Returns the
+        device bucket (keep it alive with the row) and the device pointer of each segment
+        (0 where absent) — no per-tensor views are made."""
+        elem = dtype.itemsize
+        offs, padded = layout.padded_offsets(elem)
+        host, i, key = self._slot(dtype, padded)
+        n = len(ptrs)
+        _native.check(self._lib.fedavg_host_pack(
+            ctypes.c_void_p(host.data_ptr()), (ctypes.c_void_p * n)(*ptrs),
+            (ctypes.c_int64 * n)(*[m * elem if m > 0 else 0 for m in numels]),
+            (ctypes.c_int64 * n)(*[o * elem for o in offs]), n))
+        stream = torch.cuda.current_stream(self.device)
+        bucket = torch.empty(padded, dtype=dtype, device=self.device)
+        bucket.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._events[key][i] = ev
+        self.bytes_moved += padded * elem
+        base = bucket.data_ptr()
+        return bucket, [base + o * elem if m >= 0 else 0 for o, m in zip(offs, numels)]

@@ -82,3 +82,27 @@ def test_native_delta_staging_matches_python_staging(hip_device, monkeypatch):
     assert list(native) == list(python)
     for n in native:
         assert bits_equal(native[n].numpy(), python[n].numpy()), n
+
+
+@pytest.mark.parametrize("wave", [1, 3, 64])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+def test_native_host_staging_bit_identical(hip_device, wave, dtype):
+    # whole updates in host memory (what the reference server receives): checked natively,
+    # packed into the pinned ring and moved by one DMA per client, folded from the bucket
+    g = torch.Generator().manual_seed(11)
+    rng = np.random.default_rng(11)
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=wave)
+    oracle = OracleFedAvg()
+    for k in range(8):
+        p = {n: torch.randn(s, generator=g).to(dtype) for n, s in SHAPES.items()}
+        w = int(rng.integers(100, 5000))
+        algo.process_worker_data(k, ParameterMessage(parameter=dict(p), aggregation_weight=w))
+        oracle.process_worker_data(k, OracleMessage(
+            parameter={n: (t.view(torch.int16).numpy().view(np.uint16) if dtype == torch.bfloat16 else t.numpy())
+                       for n, t in p.items()},
+            aggregation_weight=w, dtype="bfloat16" if dtype == torch.bfloat16 else None))
+    got = algo.aggregate_worker_data().parameter
+    want = oracle.aggregate_worker_data().parameter
+    assert list(got) == list(want)
+    for n, v in want.items():
+        assert bits_equal(got[n].cpu().numpy(), v), n

@@ -7,6 +7,7 @@ from __future__ import annotations
 import importlib.machinery
 import importlib.util
 import os
+import warnings
 from types import ModuleType
 
 import torch  # noqa: F401  (the extension links against torch's libraries)
@@ -22,10 +23,14 @@ def module() -> ModuleType | None:
     if not _tried:
         _tried = True
         if STAGING_PATH.exists() and os.environ.get("FEDAVG_PY_STAGING") != "1":
-            loader = importlib.machinery.ExtensionFileLoader(STAGING_NAME, str(STAGING_PATH))
-            spec = importlib.util.spec_from_file_location(STAGING_NAME, str(STAGING_PATH), loader=loader)
-            assert spec is not None
-            mod = importlib.util.module_from_spec(spec)
-            loader.exec_module(mod)
-            _module = mod
+            try:
+                loader = importlib.machinery.ExtensionFileLoader(STAGING_NAME, str(STAGING_PATH))
+                spec = importlib.util.spec_from_file_location(STAGING_NAME, str(STAGING_PATH), loader=loader)
+                assert spec is not None
+                mod = importlib.util.module_from_spec(spec)
+                loader.exec_module(mod)
+                _module = mod
+            except (ImportError, OSError) as e:  # e.g. built against another torch: stage in Python
+                warnings.warn(f"staging extension {STAGING_PATH} not loadable ({e}); staging in Python",
+                              RuntimeWarning, stacklevel=2)
     return _module

@@ -66,6 +66,8 @@ from .aggregation_algorithm import (
 
 _KERNEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
 _STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # staging_ext.cpp codes
+# host QSGD records packed by pointer (FEDAVG_QSGD_HOST_PTRS=0: through per-record views, A/B knob)
+_HOST_RECORD_PTRS = os.environ.get("FEDAVG_QSGD_HOST_PTRS", "1") != "0"
 
 
 def _is_elementwise(weight: Any, parameter: Any) -> bool:
@@ -452,6 +454,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 ptrs.append(0)
                 nums.append(-1)
         resident = False
+        q_row: tuple | None = None  # (device pointers, record bytes, keep) of packed host records
         if in_place and len(dtypes) == 1 and next(iter(dtypes)) in _KERNEL_DTYPES:
             dt = next(iter(dtypes))
             resident = True
@@ -463,7 +466,14 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             if codecs and len(codecs) == 1 and all(isinstance(t, QuantizedTensor) for t in present) and not ew:
                 # quantised update: the records are the kernel operands (dequantised in the fold)
                 dt = codecs.pop()
-                tensors = self._records_to_device(tensors)
+                recs = [None if t is None else t.record for t in tensors]
+                if _HOST_RECORD_PTRS and not self.eager_nan_check and \
+                        all(r is None or (r.device.type == "cpu" and r.is_contiguous()) for r in recs):
+                    # host records: packed from their pointers, one DMA, row pointers from the
+                    # bucket offsets (no per-record views, no second per-record pass)
+                    q_row = self._host_records_to_device(tensors, recs)
+                else:
+                    tensors = self._records_to_device(tensors)
             else:
                 if codecs:  # mixed with dense tensors (e.g. complete()-d keys): dequantise here
                     tensors = [dequantize_tensor(t) if isinstance(t, QuantizedTensor) else t for t in tensors]
@@ -485,6 +495,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self.__table_delta = delta
         if resident and not self.__ew:
             self.__table.add_resident_client(ptrs, weights, nums, dt.itemsize, dev_idx, keep)
+        elif q_row is not None:
+            self.__table.add_resident_client(q_row[0], weights, q_row[1], 1, dev_idx, q_row[2])
         else:
             self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
         self.__has_data = True
@@ -529,6 +541,20 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     # Quantised updates (StochasticQuantServerEndpoint, quantized_endpoint.py:69-77,102-111) are
     # handed over as QSGD records; the kernel dequantises them inside the fold.
     accepts_quantized_messages = True
+
+    def _host_records_to_device(self, tensors: list, recs: list) -> tuple[list[int], list[int], list]:
+        """One client's host QSGD records through the pinned ingest by pointer (HostIngest
+        .to_device_pointers): (device pointers, record bytes (-1 absent), [bucket])."""
+        if self.__ingest is None:
+            self.__ingest = HostIngest(self.device)
+        numels = tuple(1 if q is None else q.numel for q in tensors)
+        rl = self.__record_layouts.get(numels)
+        if rl is None:
+            rl = self.__record_layouts[numels] = record_layout(list(numels))
+        nums = [-1 if r is None else r.numel() for r in recs]
+        bucket, dptrs = self.__ingest.to_device_pointers(rl, [0 if r is None else r.data_ptr() for r in recs],
+                                                         nums, torch.uint8)
+        return dptrs, nums, [bucket]
 
     def _records_to_device(self, tensors: list) -> list[torch.Tensor | None]:
         """One client's QSGD records in HBM: host records go through the pinned ingest (one

@@ -864,12 +864,51 @@ constexpr int kQsgdTable = 256;  // entries per client (|p| per slot value)
 constexpr int kQsgdLanes = 256;
 constexpr int kQsgdAE = 16;
 
+// RN(1/level) for the codec levels 1..255 in both codec dtypes (constant-folded: IEEE division),
+// the reciprocal of the table build's division (exact_div.h: the correction step makes the
+// quotient correctly rounded, so each table entry keeps the reference's bits).
+struct QsgdRcp {
+  float f[256];
+  double d[256];
+};
+constexpr QsgdRcp make_qsgd_rcp() {
+  QsgdRcp t{};
+  for (int i = 1; i < 256; ++i) {
+    t.f[i] = 1.0f / static_cast<float>(i);
+    t.d[i] = 1.0 / static_cast<double>(i);
+  }
+  return t;
+}
+__constant__ QsgdRcp kQsgdRcp = make_qsgd_rcp();
+
+__device__ __forceinline__ float fma_dq(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_dq(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+template <typename DQ>
+__device__ __forceinline__ DQ qsgd_div_level(DQ a, int level) {
+#if FEDAVG_FAST_DIV
+  const DQ L = static_cast<DQ>(level);
+  constexpr DQ kLo = sizeof(DQ) == 4 ? 0x1p-100f : 0x1p-900;
+  constexpr DQ kHi = sizeof(DQ) == 4 ? 0x1p100f : 0x1p900;
+  const DQ m = __builtin_fabs(a);
+  if (__builtin_expect(level >= 1 && level <= 255 && m <= kHi && (m >= kLo || a == DQ(0)), 1)) {
+    const DQ y = sizeof(DQ) == 4 ? static_cast<DQ>(kQsgdRcp.f[level]) : static_cast<DQ>(kQsgdRcp.d[level]);
+    const DQ q0 = a * y;
+    const DQ t = fma_dq(q0, L, -a);  // exact residual, negated (keeps the sign of 0 / L)
+    return fma_dq(-t, y, q0);
+  }
+  return a / L;  // lanes outside the proven range (exec-masked: skipped when no lane needs it)
+#else
+  return a / static_cast<DQ>(level);
+#endif
+}
+
 template <typename DQ>
 __device__ __forceinline__ double qsgd_product(double norm, int level, int slot, double w) {
   // torch evaluates `norm * sign * slot / level` left to right in the codec's dtype; with
   // sign = +1 the first product is exact, so the non-negative value is (norm * slot) / level.
   const DQ n = static_cast<DQ>(norm);
-  const DQ v = (n * static_cast<DQ>(slot)) / static_cast<DQ>(level);
+  const DQ v = qsgd_div_level<DQ>(n * static_cast<DQ>(slot), level);
   const double x = static_cast<double>(v);  // .to(float64), fed_avg_algorithm.py:54
   return x * w;
 }

@@ -22,6 +22,14 @@ duration from HIP events recorded on the launch stream inside the timed region. 
 sample of the same workload, rank 0, N=1 only.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Launch. ``--gpus N > 1`` without ``WORLD_SIZE`` in the environment makes this process a
+launcher that never touches the GPU: it starts N fresh rank processes of this script (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT), forwards their stderr,
+relays rank 0's single JSON line and exits non-zero if any rank fails or outlives
+``--launch-timeout`` — the reference's simulator likewise starts its own worker processes
+(simulation_lib/task.py:142-185, context.py:215-230). Under ``torch.distributed.run`` (WORLD_SIZE
+set) the ranks are already there and nothing is spawned.
 """
 
 from __future__ import annotations
@@ -33,9 +41,110 @@ import sys
 import time
 from pathlib import Path
 
-import numpy as np
-import torch
-import torch.distributed as dist
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def _launch_ranks(argv: list[str]) -> int | None:
+    """Spawn the ranks of a ``--gpus N`` run when no launcher did (see the module docstring).
+
+    Returns the exit code for this (parent) process, or None when this process is itself a rank
+    (or a one-GPU run) and should go on to main(). Only the standard library is used here: the
+    parent imports neither torch nor the package, so it never initialises the GPU and the
+    children start from a clean process (no fork of a HIP runtime)."""
+    import signal
+    import subprocess
+    import threading
+
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--launch-timeout", type=float, default=1200.0)
+    known, _ = pre.parse_known_args(argv)
+    if known.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    n = known.gpus
+    port = _free_port()
+    procs: list[subprocess.Popen] = []
+    base = dict(os.environ)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                GROUP_RANK="0", BENCH_LAUNCHED_BY="bench.py")
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(
+            [sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+            stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, stderr=None, text=True,
+            start_new_session=True))  # own process group: the parent can stop a rank and its children
+    json_lines: list[str] = []
+
+    def relay() -> None:  # rank 0's stdout: the JSON line is kept, anything else goes to stderr
+        assert procs[0].stdout is not None
+        for line in procs[0].stdout:
+            if line.lstrip().startswith("{"):
+                json_lines.append(line.strip())
+            else:
+                sys.stderr.write(line)
+
+    reader = threading.Thread(target=relay, daemon=True)
+    reader.start()
+
+    def stop_all() -> None:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_kill = time.monotonic() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    deadline = time.monotonic() + known.launch_timeout
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with status {bad[0][1]}"
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            failed = f"ranks still running after --launch-timeout {known.launch_timeout:g} s"
+            break
+        time.sleep(0.2)
+    if failed:
+        stop_all()
+        reader.join(timeout=5.0)
+        print(f"bench.py launcher: {failed}; stopped all {n} ranks", file=sys.stderr)
+        return 1
+    reader.join(timeout=30.0)
+    if len(json_lines) != 1:
+        print(f"bench.py launcher: rank 0 printed {len(json_lines)} JSON lines (expected 1)", file=sys.stderr)
+        return 1
+    print(json_lines[0], flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    _rc = _launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        raise SystemExit(_rc)
+
+import numpy as np  # noqa: E402  (after the launcher: the parent of a --gpus N run never imports torch)
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
@@ -528,8 +637,7 @@ def main_elements(args: argparse.Namespace) -> int:
     device = torch.device("cuda", 0 if args.rehearse else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        _rendezvous_env()
         if args.rehearse:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
@@ -634,6 +742,88 @@ def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -
     return float(d["hbm_traffic_bytes_per_launch"]), f"profiles/{files[-1].name}"
 
 
+def job_clients(args: argparse.Namespace, world: int) -> int:
+    """Clients of the whole job: BASELINE.json configs[2] (256 over the GPUs) at N > 1, configs[1]
+    (--clients-per-gpu = 64) on one GPU; --weak keeps --clients-per-gpu on every rank."""
+    if args.weak:
+        return args.clients_per_gpu * world
+    if args.total_clients > 0:
+        return args.total_clients
+    return 256 if world > 1 else args.clients_per_gpu
+
+
+def shard_bounds(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous client shards: rank r folds clients [lo, hi) (N/G each; the dispatcher's split)."""
+    return rank * n_total // world, (rank + 1) * n_total // world
+
+
+def workload_name(args: argparse.Namespace, world: int, n_total: int, n_waves: int, wave: int) -> str:
+    short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    name = f"fedavg_{args.layout}_{short}_{n_total}_clients"
+    if world > 1:
+        name += f"_sharded_over_{world}_gpus" + ("_weak" if args.weak else "")
+    if n_waves > 1:
+        name += f"_waves_of_{wave}"
+    return name
+
+
+def _rendezvous_env() -> None:
+    """MASTER_ADDR / MASTER_PORT for a process group: the launcher's (or torchrun's) when set,
+    else 127.0.0.1 and a free port (a one-rank --force-collective run)."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(_free_port())
+
+
+def main_dry(args: argparse.Namespace) -> int:
+    """--dry-run: the multi-rank skeleton of main() on the CPU — gloo group, client shards, a
+    barrier-bracketed timed region of empty steps, max over ranks, one JSON line from rank 0."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        _rendezvous_env()
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    layout = LAYOUTS[args.layout]()
+    n_total = job_clients(args, world)
+    lo, hi = shard_bounds(n_total, world, rank)
+    if hi - lo < 1:
+        raise SystemExit(f"{n_total} clients cannot be sharded over {world} ranks")
+    wave = args.wave if 0 < args.wave < hi - lo else hi - lo
+    n_waves = -(-(hi - lo) // wave)
+    shards = torch.tensor([lo, hi], dtype=torch.int64)
+    if world > 1:
+        gathered = [torch.empty(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, shards)
+        dist.barrier()
+    else:
+        gathered = [shards]
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return 0
+    line = {
+        "metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+        "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "dry run: no client data, no GPU work",
+        "config": {"workload": workload_name(args, world, n_total, n_waves, wave), "total_clients": n_total,
+                   "params_per_client": layout.total_numel, "tensors_per_client": layout.num_segments,
+                   "client_shards": [[int(a), int(b)] for a, b in (g.tolist() for g in gathered)],
+                   "launched_by": os.environ.get("BENCH_LAUNCHED_BY", "external launcher" if world > 1 else "none")},
+        "dry_run": "launcher check on the CPU: rank processes, gloo group, shards, max-over-ranks timing; "
+                   "not a measurement",
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -681,7 +871,16 @@ def main() -> int:
                     help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU); "
                          "qsgd: FedAvg over QSGD-quantised updates, dequantisation fused (one GPU)")
     ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
+    ap.add_argument("--launch-timeout", type=float, default=1200.0,
+                    help="--gpus N > 1 without an external launcher: seconds before the spawned ranks are "
+                         "stopped and the run fails")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group, takes its client "
+                         "shard and the max-over-ranks timing of an empty step; prints the JSON line "
+                         "with value null (no measurement)")
     args = ap.parse_args()
+    if args.dry_run:
+        return main_dry(args)
     if args.workload == "personalized":
         return main_personalized(args)
     if args.workload == "qsgd":
@@ -700,13 +899,11 @@ def main() -> int:
     device = torch.device("cuda", 0 if args.rehearse else local_rank)
     torch.cuda.set_device(device)
     if args.rehearse and (world > 1 or args.force_collective):
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        _rendezvous_env()
         dist.init_process_group("gloo", rank=rank, world_size=world)
         args.comm = "torch"
     elif world > 1 or args.force_collective:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        _rendezvous_env()
         # RCCL on a high-priority stream: its workgroups take free CU slots ahead of the next
         # chunk's partial-kernel workgroups, so the reduce of chunk c starts under chunk c+1
         opts = dist.ProcessGroupNCCL.Options()
@@ -722,15 +919,8 @@ def main() -> int:
     layout = LAYOUTS[args.layout]()
     P = layout.total_numel
     T = layout.num_segments
-    if args.weak:
-        n_total = args.clients_per_gpu * world
-    elif args.total_clients > 0:
-        n_total = args.total_clients
-    else:
-        # BASELINE.json configs[2] (256 clients over the GPUs) / one GPU: configs[1] (64 clients)
-        n_total = 256 if world > 1 else args.clients_per_gpu
-    # contiguous client shards: rank r folds clients [lo, hi) (N/G each; the dispatcher's split)
-    lo, hi = rank * n_total // world, (rank + 1) * n_total // world
+    n_total = job_clients(args, world)
+    lo, hi = shard_bounds(n_total, world, rank)
     n_local = hi - lo
     if n_local < 1:
         raise SystemExit(f"{n_total} clients cannot be sharded over {world} ranks")
@@ -887,12 +1077,7 @@ def main() -> int:
         dist.destroy_process_group()
     if rank != 0:
         return 0
-    short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
-    workload = f"fedavg_{args.layout}_{short}_{n_total}_clients"
-    if world > 1:
-        workload += f"_sharded_over_{world}_gpus" + ("_weak" if args.weak else "")
-    if n_waves > 1:
-        workload += f"_waves_of_{wave}"
+    workload = workload_name(args, world, n_total, n_waves, wave)
     if args.layout == "resnet18" and not args.weak and n_total == 64 and world == 1:
         baseline_config = "BASELINE.json configs[1]"
     elif args.layout == "resnet18" and not args.weak and n_total == 256:

@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 from .fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from . import _native
+from .sharded import union_flags
 
 RANGE_ALIGN = 4096  # range boundaries fall on multiples of this many elements (16-B aligned views)
 _FLAG_LOCAL_ERROR = 0x100  # a rank's fold raised (e.g. nothing to aggregate): every rank raises
@@ -171,22 +172,19 @@ def range_sharded_reduce(
     if world != shard.world:
         raise ValueError(f"the shard was cut for {shard.world} ranks, the group has {world}")
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    if rank == root:
-        if out is None or out.numel() != shard.layout.total_numel or out.dtype != out_dtype or not out.is_contiguous():
-            raise ValueError("the root needs a contiguous flat output of the layout's size and dtype")
-    # a rank whose fold fails still joins the flag reduction below, so no rank waits forever
+    # a rank whose fold fails — or a root without a usable output — still joins the flag
+    # reduction below, so no rank waits forever in a collective the failing rank never reaches
     error: Exception | None = None
     try:
+        if rank == root and (out is None or out.numel() != shard.layout.total_numel or out.dtype != out_dtype
+                             or not out.is_contiguous()):
+            raise ValueError("the root needs a contiguous flat output of the layout's size and dtype")
         local = shard.fold(table, in_dtype, out_dtype)
         flags = shard.flags()
     except (RuntimeError, ValueError) as e:
         error, local, flags = e, torch.empty(0, dtype=out_dtype, device=shard.device), _FLAG_LOCAL_ERROR
     if world > 1:
-        host = dist.get_backend(group) == "gloo"
-        on_host = host or shard.device is None or torch.device(shard.device).type != "cuda"
-        f = torch.tensor([flags], dtype=torch.int32, device="cpu" if on_host else shard.device)
-        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
-        global_flags = int(f.item())
+        global_flags = union_flags(flags, group, shard.device)
     else:
         global_flags = flags
     if global_flags & _FLAG_LOCAL_ERROR:

@@ -46,7 +46,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native
-from .fedavg import ClientTable, FedAvgContext, OutputTable
+from .fedavg import ClientTable, FedAvgContext, NaNAggregationError, OutputTable
 
 
 EXCHANGES = ("auto", "reduce", "scatter")
@@ -54,6 +54,32 @@ EXCHANGES = ("auto", "reduce", "scatter")
 # exchange keeps up with the fold); the first chunk half the others (the exchange starts sooner
 # when it does not)
 CHUNK_SHAPES = ("even", "taper", "ramp")
+
+
+FLAG_BITS = 16  # NaN flag words are bit sets: FLAG_ACC_NAN / RESULT / CENTRAL, local-error bits above
+
+
+def union_flags(flags: int, group: dist.ProcessGroup | None = None, device: torch.device | str | None = None) -> int:
+    """Bitwise OR of every rank's flag word (collective over ``group``).
+
+    The backends reduce with SUM / MAX / MIN only, so each bit travels as its own int32 and the
+    bits are MAX-reduced: every rank gets the union, e.g. FLAG_ACC_NAN from one rank and
+    FLAG_RESULT_NAN from another give both, and every rank raises the same (first) assertion."""
+    if not 0 <= flags < (1 << FLAG_BITS):
+        raise ValueError(f"flag word {flags:#x} outside {FLAG_BITS} bits")
+    on_host = device is None or dist.get_backend(group) == "gloo" or torch.device(device).type != "cuda"
+    bits = torch.tensor([(flags >> b) & 1 for b in range(FLAG_BITS)], dtype=torch.int32,
+                        device="cpu" if on_host else device)
+    dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=group)
+    return sum(1 << b for b, v in enumerate(bits.tolist()) if v)
+
+
+def raise_for_flags(flags: int, where: str) -> None:
+    """The reference's assertion for a flag word that another rank raised (fed_avg_algorithm.py:93 / :97)."""
+    if flags & _native.FLAG_ACC_NAN:
+        raise NaNAggregationError("accumulator", f"NaN in the weighted sum ({where}: an input or inf - inf)")
+    if flags:
+        raise NaNAggregationError("result", f"NaN after dividing by the total weight ({where})")
 
 
 def resolve_exchange(exchange: str, world: int) -> str:
@@ -89,6 +115,8 @@ class LocalReducer(Protocol):
     def finalize_window(self, src: torch.Tensor, lo: int, hi: int, res: torch.Tensor) -> None: ...
 
     def copy_out(self, res: torch.Tensor) -> None: ...
+
+    def nan_flags(self) -> int: ...
 
     def raise_on_nan(self) -> None: ...
 
@@ -218,6 +246,10 @@ class HipLocalReducer:
         assert self._finalize_plan is not None, "set_accumulated first"
         self._finalize_plan.copy_out(res)
 
+    def nan_flags(self) -> int:
+        """This rank's latched NaN flag bits (drains the stream; does not clear them)."""
+        return self.ctx.flags()
+
     def raise_on_nan(self) -> None:
         """The reference's NaN assertions (fed_avg_algorithm.py:35,93,97) on this rank's flags."""
         self.ctx.raise_on_nan([(t, self.in_dtype) for t in [*self.prior_waves, self.table] if t is not None])
@@ -322,9 +354,10 @@ def sharded_reduce(
     (the library's own RCCL communicator) a HIP reducer runs the whole round in one native call
     (``fedavg_sharded_round[_scatter]``); otherwise the exchange goes through
     ``torch.distributed``. ``shape`` is the chunk shape (``CHUNK_SHAPES``). ``root`` is a rank of
-    ``group``. With ``check_nan`` the root raises
-    the reference's NaN assertions (fed_avg_algorithm.py:35,93,97) before returning; under the
-    scatter exchange another rank's failed window reaches the root as a result NaN.
+    ``group``. With ``check_nan`` every rank raises the reference's NaN assertions
+    (fed_avg_algorithm.py:35,93,97) before returning when any rank's flags are set (one small
+    all-reduce of the flag bits; the root raises the precise stage). Without it the caller reads
+    the flags itself (``reducer.raise_on_nan`` / ``nan_flags``) and owns the agreement.
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1 and not (force_collective and dist.is_initialized()):
@@ -353,8 +386,16 @@ def sharded_reduce(
             _scatter_exchange(reducer, global_totals, bounds, world, rank, root, root_global, group, host_staged)
         else:
             _reduce_exchange(reducer, global_totals, bounds, rank, root, root_global, group, host_staged)
-    if check_nan and rank == root:
-        reducer.raise_on_nan()
+    if check_nan:
+        # every rank raises together: the flag words (the root's finalize; under the scatter
+        # exchange each rank's window finalize too) are OR-ed across ranks before anyone raises,
+        # so no rank returns normally and then waits in the next round's collectives
+        dev = acc.device if acc.is_cuda and not host_staged else None
+        flags = union_flags(reducer.nan_flags(), group, dev)
+        if flags:
+            if rank == root:
+                reducer.raise_on_nan()  # the reference's stage, naming the root's own clients
+            raise_for_flags(flags, f"reported by the sharded round on rank {rank}")
     return global_totals
 
 

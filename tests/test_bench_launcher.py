@@ -1,0 +1,91 @@
+"""bench.py --gpus N without an external launcher spawns its own N rank processes (CPU, gloo).
+
+The driver's multi-GPU command may be `python3 bench.py --gpus N`; the bench must then start
+the N ranks itself (as the reference's simulator starts its workers, simulation_lib/task.py:142-185)
+instead of measuring one rank. --dry-run runs the multi-rank skeleton without a GPU.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _run(*args: str, timeout: float = 240.0) -> subprocess.CompletedProcess:
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run([sys.executable, str(REPO / "bench.py"), *args], cwd=REPO, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_lines(out: str) -> list[dict]:
+    return [json.loads(l) for l in out.splitlines() if l.strip().startswith("{")]
+
+
+@pytest.mark.parametrize("world, shards", [
+    (2, [[0, 128], [128, 256]]),
+    (3, [[0, 85], [85, 170], [170, 256]]),
+])
+def test_launcher_spawns_ranks_and_relays_one_line(world, shards):
+    r = _run("--gpus", str(world), "--dry-run", "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == world
+    assert line["config"]["workload"] == f"fedavg_resnet18_fp32_256_clients_sharded_over_{world}_gpus"
+    assert line["config"]["total_clients"] == 256
+    assert line["config"]["client_shards"] == shards
+    assert line["config"]["launched_by"] == "bench.py"
+    assert line["scaling"] == "strong" and line["steps"] == 3 and line["warmup"] == 1
+
+
+def test_one_gpu_runs_in_process():
+    r = _run("--gpus", "1", "--dry-run", "--steps", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["n_gpus"] == 1
+    assert line["config"]["workload"] == "fedavg_resnet18_fp32_64_clients"
+    assert line["config"]["launched_by"] == "none"
+
+
+def test_failing_rank_fails_the_run():
+    # every rank rejects the layout in its own argument parser: the launcher must exit non-zero
+    # and relay no JSON line
+    r = _run("--gpus", "2", "--dry-run", "--layout", "no_such_layout")
+    assert r.returncode != 0
+    assert _json_lines(r.stdout) == []
+    assert "exited with status" in r.stderr
+
+
+def test_launch_timeout_stops_the_ranks():
+    r = _run("--gpus", "2", "--dry-run", "--launch-timeout", "0.05")
+    assert r.returncode != 0
+    assert _json_lines(r.stdout) == []
+    assert "launch-timeout" in r.stderr
+
+
+def test_external_launcher_is_respected():
+    # the driver's torch.distributed.run form: WORLD_SIZE is set, bench.py spawns nothing
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.setdefault("OMP_NUM_THREADS", "1")
+    sys.path.insert(0, str(REPO))
+    from bench import _free_port
+
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        str(REPO / "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["n_gpus"] == 2
+    assert line["config"]["launched_by"] == "external launcher"
+    assert line["config"]["workload"] == "fedavg_resnet18_fp32_256_clients_sharded_over_2_gpus"

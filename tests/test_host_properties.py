@@ -1,5 +1,5 @@
-"""CPU property tests (hypothesis) of host-side pieces: the native host packer, layouts, the
-composite plugin. No GPU and no compute kernels: runs in the CPU suite."""
+"""CPU property tests (hypothesis) of host-side pieces: the native host packer, layouts. No GPU
+and no compute kernels: runs in the CPU suite."""
 
 from __future__ import annotations
 
@@ -12,11 +12,8 @@ from hypothesis import given, settings
 from hypothesis import strategies as st
 
 from distributed_learning_simulation_lib_amd import ParameterMessage, _native
-from distributed_learning_simulation_lib_amd.algorithm import CompositeAggregationAlgorithm
 from distributed_learning_simulation_lib_amd.build import build
 from distributed_learning_simulation_lib_amd.fedavg import ModelLayout
-from tests.golden_io import bits_equal
-from tests.helpers import OracleAlgorithm
 
 
 @pytest.fixture(scope="module")
@@ -61,54 +58,3 @@ def test_padded_offsets_are_aligned_and_disjoint(shapes, elem):
     ends = [o + n for o, n in zip(offs, lay.numels)]
     assert all(o * elem % 16 == 0 for o in offs)
     assert all(e <= o2 for e, o2 in zip(ends, offs[1:])) and (not ends or ends[-1] <= total)
-
-
-class _Refuses:
-    """A member that declines every arrival (process_worker_data -> False)."""
-
-    def __init__(self):
-        self.calls = []
-
-    def set_config(self, config):
-        self.calls.append("config")
-
-    def set_old_parameter(self, old_parameter):
-        self.calls.append("old")
-
-    def process_worker_data(self, worker_id, worker_data):
-        return False
-
-    def clear_worker_data(self):
-        self.calls.append("clear")
-
-    def exit(self):
-        self.calls.append("exit")
-
-
-def test_composite_forwards_like_the_reference():
-    """composite_aggregation_algorithm.py:22-69: the first accepting member handles the round."""
-    first, second = _Refuses(), OracleAlgorithm()
-    comp = CompositeAggregationAlgorithm()
-    comp.append_algorithm(second)
-    comp.prepend_algorithm(first)
-    comp.set_config("cfg")
-    comp.set_old_parameter({"a": torch.zeros(3, dtype=torch.float64)})
-    assert first.calls == ["config", "old"] and second.config == "cfg" and second.old is not None
-    xs = [torch.randn(5, generator=torch.Generator().manual_seed(i)) for i in range(3)]
-    for i, x in enumerate(xs):
-        assert comp.process_worker_data(i, ParameterMessage(parameter={"a": x}, aggregation_weight=i + 1))
-    res = comp.aggregate_worker_data()
-    acc = sum(x.double() * (i + 1) for i, x in enumerate(xs)) / 6
-    assert bits_equal(res.parameter["a"].numpy(), acc.numpy()) or np.allclose(res.parameter["a"].numpy(), acc.numpy(), rtol=1e-15)
-    comp.clear_worker_data()
-    comp.exit()
-    assert first.calls[-2:] == ["clear", "exit"]
-    with pytest.raises(AssertionError):
-        comp.aggregate_worker_data()  # nobody is handling a round
-
-
-def test_composite_raises_when_nobody_accepts():
-    comp = CompositeAggregationAlgorithm()
-    comp.append_algorithm(_Refuses())
-    with pytest.raises(NotImplementedError):
-        comp.process_worker_data(0, ParameterMessage(parameter={"a": torch.zeros(1)}, aggregation_weight=1))

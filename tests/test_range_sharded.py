@@ -115,17 +115,22 @@ def _clients(n, nan=None):
     return clients, weights
 
 
-def _worker(rank, world, port, nan, q, failing=False):
+def _worker(rank, world, port, nan, q, failing=False, bad_out=False):
     dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         clients, weights = _clients(6, nan)
         cls = FailingRangeShard if failing else OracleRangeShard
         shard = cls(LAYOUT, world, rank, None, clients=clients, weights=weights)
         out = torch.empty(LAYOUT.total_numel, dtype=torch.float64) if rank == 0 else None
+        if bad_out and rank == 0:
+            out = torch.empty(LAYOUT.total_numel - 1, dtype=torch.float64)  # the root's output is too short
         try:
             range_sharded_reduce(shard, None, torch.float32, out, torch.float64)
         except AssertionError:
             q.put((rank, "AssertionError", None))
+            return
+        except ValueError:
+            q.put((rank, "ValueError", None))
             return
         except RuntimeError:
             q.put((rank, "RuntimeError", None))
@@ -140,11 +145,11 @@ def _port():
     return rendezvous_url()
 
 
-def _run(world, nan=None, failing=False):
+def _run(world, nan=None, failing=False, bad_out=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nan, q, failing)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nan, q, failing, bad_out)) for r in range(world)]
     for p in procs:
         p.start()
     got = {r: (st, v) for r, st, v in (q.get(timeout=120) for _ in range(world))}
@@ -167,6 +172,13 @@ def test_range_sharded_gloo_bitwise(world):
 def test_a_failed_fold_fails_every_rank_without_a_hang():
     got = _run(3, failing=True)
     assert all(st == "RuntimeError" for st, _ in got.values())
+
+
+def test_a_bad_root_output_fails_every_rank_without_a_hang():
+    # the root's output check used to raise before the flag reduction, leaving the
+    # other ranks blocked in it; now the root raises its ValueError after it, the others a RuntimeError
+    got = _run(2, bad_out=True)
+    assert got[0][0] == "ValueError" and got[1][0] == "RuntimeError"
 
 
 def test_range_sharded_nan_fails_every_rank():

@@ -87,6 +87,11 @@ class TorchCPUReducer:
         for s_, (o, n) in enumerate(zip(self.acc_off, self.layout.numels)):
             self.outs[s_][:] = res[o : o + n]
 
+    def nan_flags(self):
+        if self.outs is not None and any(bool(o.isnan().any()) for o in self.outs):
+            return 0x1  # FLAG_ACC_NAN: an input NaN leaves the sum NaN
+        return 0
+
     def raise_on_nan(self):
         if self.outs is not None:
             assert not any(bool(o.isnan().any()) for o in self.outs), "NaN in the aggregate"
@@ -179,7 +184,9 @@ def test_single_rank_uses_the_fused_path():
         np.testing.assert_allclose(outs[s].numpy(), want, rtol=1e-14)
 
 
-def _nan_worker(rank, world, port, exchange, q):
+def _nan_worker(rank, world, port, exchange, q, tune=False):
+    from distributed_learning_simulation_lib_amd.sharded import exchange_candidates, tune_exchange
+
     dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         clients, weights = make_all_clients(4)
@@ -190,27 +197,60 @@ def _nan_worker(rank, world, port, exchange, q):
         red = TorchCPUReducer(LAYOUT, [clients[i] for i in mine], [weights[i] for i in mine], outs)
         local = [sum(weights[i][s] for i in mine) for s in range(LAYOUT.num_segments)]
         try:
-            sharded_reduce(red, local, chunks=2, exchange=exchange)
+            if tune:
+                tune_exchange(red, local, exchange_candidates(2), rounds=1)
+            else:
+                sharded_reduce(red, local, chunks=2, exchange=exchange)
             q.put((rank, "no error"))
         except AssertionError:
             q.put((rank, "AssertionError"))
+        # a round after the error still completes on every rank (no rank is left in a collective)
+        dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["reduce", "scatter"])
-def test_root_raises_on_a_nan_in_another_shard(exchange):
+@pytest.mark.parametrize("exchange, tune", [("reduce", False), ("scatter", False), ("auto", True)])
+def test_every_rank_raises_on_a_nan_in_another_shard(exchange, tune):
+    # only the root used to raise; the other ranks went on into the next round's
+    # collectives and waited there forever (tune_exchange checks NaN on every round)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_nan_worker, args=(r, world, port, exchange, q)) for r in range(world)]
+    procs = [ctx.Process(target=_nan_worker, args=(r, world, port, exchange, q, tune)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
-    assert got[0] == "AssertionError"  # the root sees the NaN (fed_avg_algorithm.py:35/93/97)
+        assert p.exitcode == 0
+    assert got == {0: "AssertionError", 1: "AssertionError"}  # fed_avg_algorithm.py:35/93/97
+
+
+def _union_worker(rank, world, port, q):
+    from distributed_learning_simulation_lib_amd.sharded import union_flags
+
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
+    try:
+        q.put((rank, union_flags([0x1, 0x2, 0x100][rank])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_union_flags_is_a_bitwise_or():
+    # MAX of bitmasks turned {ACC, RESULT} into RESULT on every rank
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_union_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert got == {0: 0x103, 1: 0x103, 2: 0x103}
 
 
 def _tune_worker(rank, world, port, q):

@@ -157,6 +157,7 @@ from distributed_learning_simulation_lib_amd.fedavg import (  # noqa: E402
     bw_probe,
 )
 from distributed_learning_simulation_lib_amd.sharded import (  # noqa: E402
+    ExchangeModel,
     HipLocalReducer,
     RcclComm,
     chunk_edges,
@@ -625,6 +626,93 @@ def main_qsgd(args: argparse.Namespace) -> int:
     return 0
 
 
+def main_plugin(args: argparse.Namespace) -> int:
+    """--workload plugin: the drop-in path the reference's server drives
+    (aggregation_server.py:111-145): FedAVGAlgorithm.process_worker_data x N + aggregate_worker_data
+    + clear_worker_data per round on one long-lived algorithm object, N device-resident updates of
+    named tensors (--clients-per-gpu, ResNet-18 by default), the reference's fp64 result left on the
+    device. Each round's messages are built inside its step, as the server receives them (the
+    payload tensors stay resident; ~0.4 us per message, reported within host_us_per_update)."""
+    from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMessage
+
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(device)
+    layout = LAYOUTS[args.layout]()
+    P, T, N = layout.total_numel, layout.num_segments, args.clients_per_gpu
+    in_dtype = getattr(torch, args.in_dtype)
+    out_dtype = getattr(torch, args.out_dtype)
+    buckets, views = make_clients(layout, 0, N, device, in_dtype)
+    params = [{n: v.view(s) for n, s, v in zip(layout.names, layout.shapes, row)} for row in views]
+    weights = dataset_size_weights(N)
+    wave = args.wave if args.wave > 0 else N
+    algo = FedAVGAlgorithm(device=device, wave_size=wave, result_dtype=out_dtype)
+
+    def messages() -> list:
+        return [ParameterMessage(parameter=dict(p), aggregation_weight=w) for p, w in zip(params, weights)]
+
+    host_s = [0.0]
+
+    def step() -> None:
+        h0 = time.perf_counter()
+        for wid, m in enumerate(messages()):
+            algo.process_worker_data(wid, m)
+        host_s[0] += time.perf_counter() - h0
+        res = algo.aggregate_worker_data()  # ends on the host: the NaN flags are read (:93, :97)
+        algo.clear_worker_data()
+        assert len(res.parameter) == T
+
+    for _ in range(args.warmup):
+        step()
+    ctx = algo._context()
+    ctx.prof_collect()
+    ctx.prof_enable(not args.no_kernel_events)
+    host_s[0] = 0.0
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    ctx.prof_enable(False)
+    kernel_ms, launches = ctx.prof_collect()
+    in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
+    job_bytes = N * P * in_b + P * out_b
+    n_waves = -(-N // wave)
+    launch_bytes = job_bytes + (n_waves - 1) * P * 16  # + the fp64 accumulator round trips between waves
+    step_s = elapsed / args.steps
+    kstep_s = kernel_ms * 1e-3 / args.steps
+    achieved = launch_bytes / kstep_s / 1e9 if kstep_s > 0 else 0.0
+    cpu = None
+    if not args.no_cpu_baseline:
+        del params, views, buckets
+        algo.exit()
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(layout)
+    short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    line = {
+        "metric": "aggregated GB/s (device-resident) through the plugin surface: FedAVGAlgorithm."
+                  "process_worker_data x N + aggregate_worker_data",
+        "value": round(job_bytes / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "replicas only", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
+        "config": {"workload": f"plugin_fedavg_{args.layout}_{short}_{N}_clients" + (f"_waves_of_{wave}" if n_waves > 1 else ""),
+                   "clients": N, "params_per_client": P, "tensors_per_client": T, "in_dtype": args.in_dtype,
+                   "out_dtype": args.out_dtype, "clients_per_launch": wave,
+                   "host_us_per_update": round(host_s[0] / (args.steps * N) * 1e6, 2),
+                   "process_worker_data_ms_per_round": round(host_s[0] / args.steps * 1e3, 4),
+                   "baseline_config": "BASELINE.json configs[1] through the reference's plugin call sequence"},
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": f"fedavg_tile_kernel x {n_waves} launch(es) per round", "bytes_per_step": launch_bytes,
+            "kernel_ms_per_step": round(kstep_s * 1e3, 4), "launches": launches},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main_elements(args: argparse.Namespace) -> int:
     """--shard elements: every rank folds its element range of ALL clients (range_sharded.py):
     bit-identical to one GPU at any N, the exchange is a gather of the fp32 result. The same
@@ -859,7 +947,8 @@ def main() -> int:
                     help="N > 1 with --exchange auto: take the cost model's exchange instead of timing "
                          "every (exchange, chunks) candidate before the warmup")
     ap.add_argument("--in-dtype", default="float32", choices=["float32", "float16", "bfloat16", "float64"])
-    ap.add_argument("--out-dtype", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--out-dtype", default=None, choices=["float32", "float64"],
+                    help="result dtype (default float32; float64 — the reference's — for --workload plugin)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true",
@@ -867,9 +956,10 @@ def main() -> int:
     ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
-    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd"],
+    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd", "plugin"],
                     help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU); "
-                         "qsgd: FedAvg over QSGD-quantised updates, dequantisation fused (one GPU)")
+                         "qsgd: FedAvg over QSGD-quantised updates, dequantisation fused (one GPU); "
+                         "plugin: the headline round through FedAVGAlgorithm's plugin calls (one GPU)")
     ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
     ap.add_argument("--launch-timeout", type=float, default=1200.0,
                     help="--gpus N > 1 without an external launcher: seconds before the spawned ranks are "
@@ -879,12 +969,16 @@ def main() -> int:
                          "shard and the max-over-ranks timing of an empty step; prints the JSON line "
                          "with value null (no measurement)")
     args = ap.parse_args()
+    if args.out_dtype is None:
+        args.out_dtype = "float64" if args.workload == "plugin" else "float32"
     if args.dry_run:
         return main_dry(args)
     if args.workload == "personalized":
         return main_personalized(args)
     if args.workload == "qsgd":
         return main_qsgd(args)
+    if args.workload == "plugin":
+        return main_plugin(args)
     if args.shard == "elements":
         return main_elements(args)
 
@@ -960,6 +1054,14 @@ def main() -> int:
     selection = "fixed" if args.exchange != "auto" else "cost model"
     tuned = None
     chunk_shape = "even"
+    model = ExchangeModel()
+    in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
+    if sharded and world > 1 and args.exchange == "auto" and args.no_tune:
+        # DESIGN.md §5 cost model: the (exchange, chunks, shape) with the smallest predicted step
+        (exchange, ch, chunk_shape), _ = model.best(
+            world, P, n_total, in_b, out_b, ctx.num_tiles, exchange_candidates(None if chunks_auto else args.chunks),
+            balance_root=False)
+        args.chunks = ch
     if sharded and args.exchange == "auto" and not args.no_tune:
         # time every (exchange, chunks) candidate on this node before the warmup (untimed; the
         # max over ranks decides, so every rank picks the same): the link rate the DESIGN.md §5
@@ -1078,6 +1180,8 @@ def main() -> int:
     if rank != 0:
         return 0
     workload = workload_name(args, world, n_total, n_waves, wave)
+    predicted = None if world < 2 else model.round_ms(
+        world, P, n_total, in_b, out_b, chunk_edges(ctx.num_tiles, args.chunks, chunk_shape), exchange)
     if args.layout == "resnet18" and not args.weak and n_total == 64 and world == 1:
         baseline_config = "BASELINE.json configs[1]"
     elif args.layout == "resnet18" and not args.weak and n_total == 256:
@@ -1121,6 +1225,10 @@ def main() -> int:
                 "partial_only_ms_per_step": None if partial_only_ms is None else round(partial_only_ms, 4),
                 "exposed_exchange_and_finalize_ms": (None if partial_only_ms is None
                                                      else round(step_s * 1e3 - partial_only_ms, 4)),
+                # DESIGN.md §5 cost model for this schedule (measured one-GPU rates, quoted xGMI
+                # rate x assumed RCCL efficiency): its fold / exposed terms beside the measured ones
+                "predicted_speedup": None if predicted is None else predicted["speedup"],
+                "predicted": predicted,
             },
             "baseline_config": baseline_config,
             **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not an N-GPU measurement"}

@@ -43,6 +43,7 @@ _PD = POINTER(c_double)
 SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_abi_version": (c_int32, []),
     "fedavg_build_flags": (c_int32, []),
+    "fedavg_kernel_constant": (c_int32, [ctypes.c_char_p, POINTER(c_int64)]),
     "fedavg_layout_acc_numel": (c_int64, [POINTER(c_int64), c_int32]),
     "fedavg_last_error": (ctypes.c_char_p, []),
     "fedavg_qsgd_record_bytes": (c_int64, [c_int64]),
@@ -168,7 +169,10 @@ def load(path: str | None = None, allow_ablated: bool = False) -> ctypes.CDLL:
             f"MI355X FedAvg library not loadable at {lib_path}: {e}. "
             "Build it with `python -c 'import __graft_entry__ as g; g.build()'`."
         ) from e
+    tuning_build = lib_path != str(LIB_PATH)
     for name, (restype, argtypes) in SIGNATURES.items():
+        if tuning_build and not hasattr(lib, name):
+            continue  # a tuning build from older sources: A/B runs use the timed entry points only
         fn = getattr(lib, name)
         fn.restype = restype
         fn.argtypes = argtypes
@@ -183,6 +187,13 @@ def load(path: str | None = None, allow_ablated: bool = False) -> ctypes.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def kernel_constant(name: str) -> int:
+    """A compile-time constant of the kernels' geometry (``fedavg_kernel_constant``)."""
+    v = c_int64()
+    check(load().fedavg_kernel_constant(name.encode(), ctypes.byref(v)))
+    return int(v.value)
 
 
 def last_error() -> str:

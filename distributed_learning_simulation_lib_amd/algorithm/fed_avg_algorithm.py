@@ -43,15 +43,17 @@ import numpy as np
 import torch
 
 from .. import _staging
+from .._staging import NativeClientTable
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
 from ..message import (
+    KIND_DELTA,
+    KIND_PARAMETER,
     DeltaParameterMessage,
     Message,
     ModelParameter,
     ParameterMessage,
-    is_delta_message,
-    is_parameter_message,
+    message_kind,
     wire_class,
 )
 from ..quantized import QuantizedTensor, dequantize_tensor, record_layout
@@ -66,6 +68,7 @@ from .aggregation_algorithm import (
 
 _KERNEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
 _STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # staging_ext.cpp codes
+_STAGING_CODES = {dt: code for code, dt in enumerate(_STAGING_DTYPES)}
 # host QSGD records packed by pointer (FEDAVG_QSGD_HOST_PTRS=0: through per-record views, A/B knob)
 _HOST_RECORD_PTRS = os.environ.get("FEDAVG_QSGD_HOST_PTRS", "1") != "0"
 
@@ -135,11 +138,18 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__record_layouts: dict[tuple[int, ...], ModelLayout] = {}
         # fed_avg_algorithm.py:59-62, kept with the hook's own objects (scalar weights)
         self.__host_totals: dict[str, Any] = {}
+        # while every staged update of the round carried every name of the layout, all per-name
+        # totals are one value: kept once (``__uniform_total`` after ``__uniform_count`` updates)
+        # and written into __host_totals only when an update needs per-name bookkeeping
+        self.__uniform_total: Any = None
+        self.__uniform_count = 0
+        self.__round_fresh = True  # no update of this round seen yet
         # per-element weights: decided by the round's first update
         self.__ew: bool | None = None
         # no per-tensor hook overridden: a scalar-weighted arrival is staged in one pass
         # (process_worker_data), with the default hooks' exact effect
-        self.__staging_maps: tuple | None = None  # (layout, name -> native segment, native shapes)
+        self.__result_geo: dict = {}
+        self.__fast: tuple | None = None  # _fast_maps(): (layout, name -> native segment, shapes, device)
         cls = type(self)
         self.__default_hooks = all(getattr(cls, h) is getattr(FedAVGAlgorithm, h)
                                    for h in ("_accumulate_parameter", "_get_weight", "_note_total"))
@@ -205,7 +215,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_id: int,
         worker_data: Message | None,
     ) -> bool:
-        res = super().process_worker_data(worker_id=worker_id, worker_data=worker_data)
+        res = super().process_worker_data(worker_id, worker_data)
         if not res:
             return False
         worker_data = self._all_worker_data.get(worker_id, None)
@@ -213,10 +223,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             return True
         # messages are recognised by their dataclass fields, not by class identity: the
         # reference's own server passes simulation_lib.message objects (message.py)
-        if is_delta_message(worker_data) and not (self.accumulate and self._delta_fusable(worker_data)
-                                                  and not self.__ew):
+        kind = message_kind(worker_data)
+        if kind == KIND_DELTA and not (self.accumulate and self._delta_fusable(worker_data) and not self.__ew):
             worker_data = self._restore_on_host(worker_id, worker_data)
-        if is_delta_message(worker_data):
+            kind = message_kind(worker_data)
+        if kind == KIND_DELTA:
             # restore() fused into the fold: x = old + delta in the kernel (message.py:40-61)
             assert self._old_parameter is not None
             assert len(worker_data.delta_parameter) == len(self._old_parameter)
@@ -233,15 +244,25 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             if any(_is_elementwise(w, t) for t, w in row.values()):
                 # per-element weights take the dense elementwise fold: restore first
                 worker_data = self._restore_on_host(worker_id, worker_data)
+                kind = message_kind(worker_data)
             else:
+                self._materialize_totals()
                 for name, (delta, weight) in row.items():
                     self._note_total(name, weight, delta)
                 self.__row = row
                 worker_data.delta_parameter = {}
                 self._stage_client(delta=True, worker_id=worker_id)
                 return True
-        if not is_parameter_message(worker_data):
+        if kind != KIND_PARAMETER:
             return True
+        if self.__round_fresh and self.accumulate:
+            # the reference's per-name dicts start empty every round (:55-62): the round's first
+            # update sets the names and their order (a layout equal to the last round's keeps its
+            # context); later names grow it (_grow_layout)
+            self.__round_fresh = False
+            params = worker_data.parameter
+            if isinstance(params, dict) and params and (self.__layout is None or tuple(params) != self.__layout.names):
+                self._set_layout(params)
         w = worker_data.aggregation_weight
         if self.accumulate and self.__default_hooks and isinstance(w, (int, float)):
             # the default _accumulate_parameter / _get_weight / _note_total for every tensor of
@@ -251,6 +272,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             if self._stage_natively(params, w):
                 worker_data.parameter = {}
                 return True
+            self._materialize_totals()
             totals = self.__host_totals
             for name in params:
                 if name in totals:
@@ -262,6 +284,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self._stage_client(worker_id=worker_id)
             return True
         self.__row = {}
+        self._materialize_totals()
         for name, parameter in worker_data.parameter.items():
             self._accumulate_parameter(worker_data=worker_data, name=name, parameter=parameter)
         if self.accumulate:
@@ -269,30 +292,67 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return True
 
     def _stage_natively(self, params: Any, w: Any, delta: bool = False) -> bool:
-        """The default hooks' per-tensor walk of a resident update in one native call
-        (csrc/staging_ext.cpp): per-name totals `+= w` in the update's key order, the row's device
-        pointers, the shape / device / contiguity / dtype checks; contiguous host updates of one
-        dtype are packed and moved by the pinned ingest from the pointers. ``delta``: the tensors are a
-        DeltaParameterMessage's deltas, folded with restore() fused (x = old + delta). False
-        (nothing changed) when the extension is absent or the update needs the general path."""
-        ext = _staging.module()
-        if (ext is None or self.__native_layout is None or self.__layout is None or self.__ew
-                or self.eager_nan_check or not isinstance(params, dict)):
+        """The default hooks' per-tensor walk of an update in one native call
+        (csrc/staging_ext.cpp). A device-resident update is checked (known name, contiguous, on
+        the device, one kernel dtype, the layout's shape) and written straight into the wave's
+        native client table (``Rows.append``); the per-name totals `+= w` (:59-62) take one
+        addition while every update of the round carries every name. A contiguous host update of
+        one dtype is checked, its totals updated, and it is packed and moved by the pinned ingest
+        from its pointers. ``delta``: the tensors are a DeltaParameterMessage's deltas, folded with
+        restore() fused (x = old + delta). False (nothing changed) when the extension is absent or
+        the update needs the general path."""
+        if self.__ew or not isinstance(params, dict):
             return False
-        dev = self.device
-        if dev.type != "cuda":
-            return False
-        dev_idx = dev.index if dev.index is not None else torch.cuda.current_device()
-        if self.__staging_maps is None or self.__staging_maps[0] is not self.__layout:
-            index = {n: -1 for n in self.__layout.names}
-            for j, i in enumerate(self.__keep):
-                index[self.__layout.names[i]] = j
-            shapes = [tuple(self.__layout.shapes[i]) for i in self.__keep]
-            self.__staging_maps = (self.__layout, index, shapes)
-        _, index, shapes = self.__staging_maps
+        fast = self.__fast
+        if fast is None or fast[0] is not self.__layout:
+            fast = self.__fast = self._fast_maps()
+            if fast is None:
+                return False
+        _, index, shapes, dev_idx = fast
+        if self.__table is not None and self.__table.num_clients >= self.wave_size:
+            self._flush()  # a full wave is folded when the next update arrives (see _stage_client)
+        table = self.__table
+        fresh = table is None
+        want = -1
+        if not fresh:
+            want = _STAGING_CODES.get(self.__table_dtype, -3) if type(table) is NativeClientTable else -3
+            if want == -3 or self.__table_delta != delta:
+                want = -3  # the wave so far is not a native table of this kind: general path below
+        if want != -3:
+            if fresh:
+                table = NativeClientTable(len(self.__keep), dev_idx)
+            rc = table.rows.append(params, index, shapes, w, want)
+            if rc <= -2:  # a valid update of another dtype: the wave so far is folded first
+                self._flush()
+                table, fresh = NativeClientTable(len(self.__keep), dev_idx), True
+                rc = table.rows.append(params, index, shapes, w, -1)
+            if rc >= 0:
+                if rc & 16 and not self.__host_totals:
+                    # a complete update while every total is still the same value
+                    self.__uniform_total = w if self.__uniform_count == 0 else self.__uniform_total + w
+                    self.__uniform_count += 1
+                else:
+                    self._materialize_totals()
+                    totals = self.__host_totals
+                    for name in params:
+                        if name in totals:
+                            totals[name] += w
+                        else:
+                            totals[name] = w
+                if fresh:
+                    self.__table = table
+                    self.__table_dtype = _STAGING_DTYPES[rc & 15]
+                    self.__table_delta = delta
+                self.__ew = False
+                self.__has_data = True
+                return True
         first = next(iter(params.values()), None)
         host = isinstance(first, torch.Tensor) and first.device.type == "cpu"
-        res = ext.stage_resident(params, index, shapes, -1 if host else dev_idx, self.__host_totals, w)
+        if not host and want != -3:
+            return False  # a device update the native check refused: the general path
+        self._materialize_totals()
+        res = _staging.module().stage_resident(params, index, shapes, -1 if host else dev_idx,
+                                               self.__host_totals, w)
         if res is None:
             return False
         ptrs, nums, weights, code, keep = res
@@ -308,14 +368,45 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
             self._flush()
         if self.__table is None:
-            self.__table = ClientTable(len(self.__keep))
+            self.__table = self._new_table(dev_idx)
             self.__table_dtype = dt
             self.__table_delta = delta
         self.__table.add_resident_client(ptrs, weights, nums, dt.itemsize, dev_idx, keep)
         self.__has_data = True
-        if self.__table.num_clients >= self.wave_size:
-            self._flush()
         return True
+
+    def _fast_maps(self) -> tuple | None:
+        """(layout, name -> native segment, native shapes, device index) of the native staging,
+        or None where it does not apply (no extension, no GPU device, eager NaN scans, nothing
+        native in the layout)."""
+        if (_staging.module() is None or self.__native_layout is None or self.__layout is None
+                or self.eager_nan_check):
+            return None
+        dev = self.device
+        if dev.type != "cuda":
+            return None
+        dev_idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        index = {n: -1 for n in self.__layout.names}
+        for j, i in enumerate(self.__keep):
+            index[self.__layout.names[i]] = j
+        shapes = [tuple(self.__layout.shapes[i]) for i in self.__keep]
+        return (self.__layout, index, shapes, dev_idx)
+
+    def _materialize_totals(self) -> None:
+        """Write the running total of the complete updates into every name's total (what the
+        reference's dict holds at this point: each name saw exactly those updates, in order)."""
+        if self.__uniform_count:
+            assert self.__layout is not None and not self.__host_totals
+            total = self.__uniform_total
+            self.__host_totals = {name: total for name in self.__layout.names}
+            self.__uniform_total, self.__uniform_count = None, 0
+
+    def _new_table(self, dev_idx: int) -> ClientTable | NativeClientTable:
+        """The wave's client table: native rows when the staging extension is built (scalar
+        weights), else the Python table; per-element weights always take the Python table."""
+        if not self.__ew and _staging.module() is not None and self.device.type == "cuda":
+            return NativeClientTable(len(self.__keep), dev_idx)
+        return ClientTable(len(self.__keep))
 
     def _restore_on_host(self, worker_id: int, worker_data: Any) -> Any:
         """A delta the fold cannot take (consistency-check fields, the ratio path, per-element
@@ -487,10 +578,14 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     dt = self.__table_dtype or torch.float32
         if self.eager_nan_check:
             self._scan_arrival(tensors, dt, worker_id, delta)
-        if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta):
+        # A full wave is folded when the next update arrives, not when it fills: the round's last
+        # wave then always reaches aggregate_worker_data unfolded and is folded and divided in one
+        # launch (fedavg_aggregate) instead of an accumulate launch plus a finalize pass.
+        if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta
+                                         or self.__table.num_clients >= self.wave_size):
             self._flush()
         if self.__table is None:
-            self.__table = ClientTable(len(self.__keep))
+            self.__table = self._new_table(dev_idx)
             self.__table_dtype = dt
             self.__table_delta = delta
         if resident and not self.__ew:
@@ -500,8 +595,6 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         else:
             self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
         self.__has_data = True
-        if self.__table.num_clients >= self.wave_size:
-            self._flush()
 
     def _scan_arrival(self, tensors: list, dt: Any, worker_id: int | None, delta: bool) -> None:
         """fed_avg_algorithm.py:34-35 at the arrival: one GPU scan of the staged update."""
@@ -630,10 +723,14 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 result.update(self._finish_native())
         finally:
             self._reset_round()
-        for i, name in enumerate(layout.names):
-            if i not in self.__keep:
-                result[name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
-        out = {name: result[name] for name in layout.names}
+        if len(self.__keep) == layout.num_segments:
+            out = result  # no zero-element tensors: the native segments are the layout, in order
+        else:
+            kept = set(self.__keep)
+            for i, name in enumerate(layout.names):
+                if i not in kept:
+                    result[name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
+            out = {name: result[name] for name in layout.names}
         if self.result_device is not None:
             out = self._move_result(out)
         return out
@@ -641,6 +738,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _reset_round(self) -> None:
         self.__has_data = False
         self.__host_totals = {}
+        self.__uniform_total, self.__uniform_count = None, 0
+        self.__round_fresh = True
         self.__ew = None
         self.__tot_fp32 = {}
 
@@ -673,16 +772,18 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__table, self.__table_dtype = None, None
         pending = [(table, dt)] if table is not None and dt is not None else []
         custom_divide = type(self)._apply_total_weight is not FedAVGAlgorithm._apply_total_weight
-        names = [layout.names[i] for i in self.__keep]
         # a 0-dim tensor (or other non-number) total: divide by the host total the reference has
-        host_divide = not self.__ew and any(not isinstance(self.__host_totals.get(n, 0), (int, float))
-                                            for n in names)
+        # (the one running total of complete updates is always a number)
+        host_divide = False
+        if not self.__ew and not (self.__uniform_count and not self.__host_totals):
+            self._materialize_totals()
+            host_divide = any(not isinstance(self.__host_totals.get(layout.names[i], 0), (int, float))
+                              for i in self.__keep)
         out_dtype = torch.float64 if custom_divide else self.result_dtype
-        flat = torch.empty(native.padded_offsets(8 if out_dtype == torch.float64 else 4)[1],
-                           dtype=out_dtype, device=self.device)
+        offs, total, shapes = self._result_geometry(out_dtype)
+        flat = torch.empty(total, dtype=out_dtype, device=self.device)
         self.__result_flat = None if custom_divide else flat
-        offs, _ = native.padded_offsets(flat.element_size())
-        outs = [flat[o : o + n] for o, n in zip(offs, native.numels)]
+        outs = OutputTable.from_flat(flat, offs, native)
         delta = self.__table_delta and table is not None
         try:
             if self.__ew:
@@ -710,33 +811,53 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     ctx.set_accumulated([1.0] * native.num_segments)
                     ctx.finalize_range(outs, torch.float64)
                 else:
-                    ctx.set_accumulated([float(self.__host_totals[n]) for n in names])
+                    ctx.set_accumulated([float(self.__host_totals[layout.names[i]]) for i in self.__keep])
                     ctx.finalize_range(outs, out_dtype)
             ctx.raise_on_nan(pending)
         except NaNAggregationError:
             ctx.reset()
             raise
         result: ModelParameter = {}
-        if custom_divide:
-            # a subclass's _apply_total_weight runs where the reference runs it — on host fp64
-            # tensors (torch's GPU division by a scalar multiplies by its reciprocal, which does
-            # not round like the reference's CPU division); one D2H copy of the weighted sums
-            host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
-            host.copy_(flat)
+        ext = _staging.module()
+        if not custom_divide:
+            # the segments as shaped views of the flat result (one native call when the staging
+            # extension is built)
+            views = ext.views(flat, offs, shapes) if ext is not None else \
+                [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+            for j, i in enumerate(self.__keep):
+                result[layout.names[i]] = views[j]
+            ctx.reset()
+            return result
+        # a subclass's _apply_total_weight runs where the reference runs it — on host fp64
+        # tensors (torch's GPU division by a scalar multiplies by its reciprocal, which does not
+        # round like the reference's CPU division); one D2H copy of the weighted sums
+        host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+        host.copy_(flat)
+        self._materialize_totals()
         for j, i in enumerate(self.__keep):
             name = layout.names[i]
-            value = outs[j].view(layout.shapes[i])
-            if custom_divide:
-                total = self._total_for(name, j)
-                if isinstance(total, torch.Tensor):
-                    total = total.cpu()
-                value = host[offs[j] : offs[j] + native.numels[j]].view(layout.shapes[i])
-                value = self._apply_total_weight(name=name, parameter=value, total_weight=total)
-                assert not value.isnan().any()  # fed_avg_algorithm.py:97
-                value = value.to(device=self.device, dtype=self.result_dtype)
-            result[name] = value
+            total = self._total_for(name, j)
+            if isinstance(total, torch.Tensor):
+                total = total.cpu()
+            value = host[offs[j] : offs[j] + native.numels[j]].view(layout.shapes[i])
+            value = self._apply_total_weight(name=name, parameter=value, total_weight=total)
+            assert not value.isnan().any()  # fed_avg_algorithm.py:97
+            result[name] = value.to(device=self.device, dtype=self.result_dtype)
         ctx.reset()
         return result
+
+    def _result_geometry(self, out_dtype: torch.dtype) -> tuple[list[int], int, list[tuple[int, ...]]]:
+        """(element offsets, flat size, shapes) of the native segments in a flat result buffer of
+        ``out_dtype`` — cached per layout, reused every round."""
+        native = self.__native_layout
+        assert native is not None and self.__layout is not None
+        key = (native, out_dtype)
+        geo = self.__result_geo.get(key)
+        if geo is None:
+            offs, total = native.padded_offsets(torch.empty((), dtype=out_dtype).element_size())
+            geo = (list(offs), int(total), [tuple(self.__layout.shapes[i]) for i in self.__keep])
+            self.__result_geo = {key: geo}
+        return geo
 
     def _total_for(self, name: str, seg: int) -> Any:
         """The total object the reference hands _apply_total_weight (fed_avg_algorithm.py:95)."""

@@ -1952,12 +1952,56 @@ int out_kind_of(int32_t out_dtype) {
 
 }  // namespace
 
+extern "C" __attribute__((visibility("hidden"))) int32_t fedavg_internal_pers_constant(const char* name, int64_t* out);
+
 extern "C" {
 
 int32_t fedavg_abi_version(void) { return FEDAVG_ABI_VERSION; }
 
 int32_t fedavg_build_flags(void) {
   return (FEDAVG_ABLATE_EPILOGUE ? FEDAVG_BUILD_ABLATE_EPILOGUE : 0) | (FEDAVG_QSGD_ABLATE ? FEDAVG_BUILD_ABLATE_QSGD : 0);
+}
+
+int32_t fedavg_kernel_constant(const char* name, int64_t* out) {
+  if (name == nullptr || out == nullptr) return fail(FEDAVG_ERR_INVALID, "null argument");
+  const std::string n(name);
+  int64_t v = -1;
+  if (n == "tile") v = kTile1;
+  else if (n == "tile_wide") v = kTileWide;
+  else if (n == "split_tile") v = kTile4;
+  else if (n == "qsgd_tile") v = kTile1;
+  else if (n == "qsgd_ae") v = kQsgdAE;
+  else if (n == "qsgd_group") v = kQsgdGroup;
+  else if (n.rfind("pers_", 0) == 0) {
+    if (fedavg_internal_pers_constant(name, &v) != FEDAVG_OK) v = -1;
+  } else {
+    const auto dsep = n.rfind('_');
+    const std::string key = dsep == std::string::npos ? n : n.substr(0, dsep);
+    const std::string d = dsep == std::string::npos ? "" : n.substr(dsep + 1);
+    auto pick = [&](auto tag) {
+      using T = decltype(tag);
+      using GW = Geo<T, 1, ((sizeof(T) < 8 || FEDAVG_F64_WIDE) && kTileWide > 0) ? kTileWide : kTile1>;
+      using G1 = Geo<T, 1, kTile1>;
+      constexpr int VPLW = GW::AE / Vec16<T>::n;
+      constexpr int CU_B = sizeof(T) == 8 ? FEDAVG_CU_BYTES_F64 : FEDAVG_CU_BYTES;
+      constexpr int GROUP = (CU_B / (VPLW * 16)) < 2 ? 2 : (CU_B / (VPLW * 16));
+      constexpr bool PIPE = (FEDAVG_PIPE >> (sizeof(T) == 2 ? 0 : sizeof(T) == 4 ? 1 : 2)) & 1;
+      constexpr int PG = (FEDAVG_PIPE_BYTES / (VPLW * 16)) < 1 ? 1 : (FEDAVG_PIPE_BYTES / (VPLW * 16));
+      if (key == "ae") v = GW::AE;
+      else if (key == "lanes") v = GW::LANES;
+      else if (key == "ae4096") v = G1::AE;
+      else if (key == "lanes4096") v = G1::LANES;
+      else if (key == "group") v = GROUP;
+      else if (key == "pipe") v = PIPE ? PG : 0;
+    };
+    if (d == "f32") pick(float{});
+    else if (d == "f16") pick(__half{});
+    else if (d == "bf16") pick(bf16_t{});
+    else if (d == "f64") pick(double{});
+  }
+  if (v < 0) return fail(FEDAVG_ERR_INVALID, std::string("unknown kernel constant ") + n);
+  *out = v;
+  return FEDAVG_OK;
 }
 
 int64_t fedavg_qsgd_sign_offset(int64_t numel) {

@@ -709,6 +709,20 @@ int32_t check_pers(const fedavg_pers* p) {
 
 }  // namespace
 
+// Geometry constants for fedavg_kernel_constant ("pers_*" names; test support).
+extern "C" __attribute__((visibility("hidden"))) int32_t fedavg_internal_pers_constant(const char* name,
+                                                                                      int64_t* out) {
+  const std::string n(name);
+  if (n == "pers_chunk") *out = kChunk;
+  else if (n == "pers_jb") *out = kJB;
+  else if (n == "pers_group") *out = kGroup;
+  else if (n == "pers_u") *out = kU;
+  else if (n == "pers_ring_stage") *out = kSC;
+  else if (n == "pers_ring_depth") *out = kD;
+  else return FEDAVG_ERR_INVALID;
+  return FEDAVG_OK;
+}
+
 extern "C" {
 
 int32_t fedavg_pers_create(fedavg_pers** out, int32_t device, const int64_t* seg_numel, int32_t num_segments) {

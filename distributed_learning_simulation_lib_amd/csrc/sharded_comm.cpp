@@ -125,8 +125,13 @@ struct fedavg_comm {
   // the root's last step (finalize / copy-out) runs on the comm stream right behind the last
   // collective instead of on the compute stream behind a cross-stream wait (FEDAVG_FINISH_ON_COMM)
   bool finish_on_comm = false;
+  // the root divides the chunks already reduced while the last chunk is still being reduced
+  // (reduce exchange, >= 2 chunks; FEDAVG_OVERLAP_FINALIZE=0 turns it off): only the last chunk's
+  // finalize follows the last collective
+  bool overlap_finalize = true;
   std::vector<hipEvent_t> chunk_events;
   hipEvent_t done = nullptr;
+  hipEvent_t head_done = nullptr;  // every chunk but the last has been reduced
   // scatter exchange scratch: reduce-scattered fp64 windows (+ the root's chunk tails) and the
   // finalized result in accumulator coordinates (output dtype)
   double* slice = nullptr;
@@ -235,10 +240,12 @@ int32_t fedavg_comm_create(fedavg_comm** out, const void* id, int32_t world, int
   c->rank = rank;
   c->device = device;
   if (const char* e = std::getenv("FEDAVG_FINISH_ON_COMM")) c->finish_on_comm = std::atoi(e) != 0;
+  if (const char* e = std::getenv("FEDAVG_OVERLAP_FINALIZE")) c->overlap_finalize = std::atoi(e) != 0;
   int lo = 0, hi = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
   if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->head_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     fedavg_comm_destroy(c);
     return fedavg_internal_fail(FEDAVG_ERR_HIP, (std::string("comm stream: ") + hipGetErrorString(e)).c_str());
@@ -262,6 +269,7 @@ int32_t fedavg_comm_destroy(fedavg_comm* c) {
   if (c->nccl) (void)rccl().comm_destroy(c->nccl);
   for (hipEvent_t ev : c->chunk_events) (void)hipEventDestroy(ev);
   if (c->done) (void)hipEventDestroy(c->done);
+  if (c->head_done) (void)hipEventDestroy(c->head_done);
   if (c->slice) (void)hipFree(c->slice);
   if (c->res) (void)hipFree(c->res);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -331,17 +339,27 @@ int32_t round_reduce(fedavg_comm* c, fedavg_ctx* ctx, fedavg_plan* partial, feda
     ncclResult_t res = rccl().reduce(acc + a, acc + a, static_cast<size_t>(b - a), ncclFloat64, ncclSum, root,
                                      c->nccl, c->stream);
     if (res != ncclSuccess) return rccl_fail(res, "ncclReduce");
+    if (k == chunks - 2) COMM_HIP_TRY(hipEventRecord(c->head_done, c->stream));
   }
-  // The compute stream goes on once the last reduce has landed (the reduces run in order); the
-  // root then divides every tile in one launch. (Dividing each chunk on the comm stream right
-  // behind its reduce was measured slower: 0.595 vs 0.566 ms per one-rank round at 4 chunks —
-  // the finalize kernels contend with the next chunk's partial for CUs and HBM.)
+  // The compute stream goes on once the reduces have landed (they run in order); the root then
+  // divides. With overlap_finalize the tiles of every chunk but the last are divided as soon as
+  // their reduces are done — on the compute stream, whose partial kernels have all been issued,
+  // while the comm stream still reduces the last chunk — so only the last chunk's division
+  // follows the last collective (the exposed tail: DESIGN.md §5 cost model). (Dividing each
+  // chunk on the comm stream right behind its reduce was measured slower: 0.595 vs 0.566 ms per
+  // one-rank round at 4 chunks — those finalize kernels contend with the next chunk's partial.)
   fedavg_internal_set_prof(ctx, 0);
   if (c->rank == root && c->finish_on_comm)
     if (int32_t st = fedavg_plan_run_range(finalize, 0, n, c->stream)) return st;
+  const bool overlap = c->rank == root && !c->finish_on_comm && c->overlap_finalize && chunks >= 2;
+  if (overlap) {
+    COMM_HIP_TRY(hipStreamWaitEvent(s, c->head_done, 0));
+    if (int32_t st = fedavg_plan_run_range(finalize, 0, edges[chunks - 1], s)) return st;
+  }
   COMM_HIP_TRY(hipEventRecord(c->done, c->stream));
   COMM_HIP_TRY(hipStreamWaitEvent(s, c->done, 0));
-  if (c->rank == root && !c->finish_on_comm) return fedavg_plan_run_range(finalize, 0, n, s);
+  if (c->rank == root && !c->finish_on_comm)
+    return fedavg_plan_run_range(finalize, overlap ? edges[chunks - 1] : 0, n, s);
   return FEDAVG_OK;
 }
 

@@ -194,10 +194,165 @@ py::list views(const at::Tensor& flat, py::list offsets, py::list shapes) {
   return out;
 }
 
+// Rows — the client table of one wave, held natively ([num_clients][T] device pointers, fp64
+// weights, element counts; references to the staged tensors). FedAVGAlgorithm appends one update
+// per arrival with append(): one pass over the update's dict that checks every tensor (known name,
+// contiguous, on the device, one kernel dtype, the layout's shape) and writes its row straight
+// into the table — no Python list per update, no second pass at launch time (the arrays are
+// already contiguous). The per-name totals (fed_avg_algorithm.py:59-62) stay with the caller:
+// append() reports whether the update carried every name of the layout, so the caller can keep
+// one running total for all names while every update is complete.
+class Rows {
+ public:
+  Rows(int64_t T, int64_t device_index) : T_(T), dev_(device_index) {
+    if (T < 1) throw std::invalid_argument("a table needs at least one segment");
+  }
+
+  // append(params, index, shapes, weight, want_code) -> int
+  //   >= 0: staged; the low 4 bits are the dtype code, bit 4 (16) is set when the update carried
+  //         every name of ``index`` (a complete update)
+  //   -1:   nothing changed — the update needs the general path
+  //   -2 - c: nothing changed — a valid update of dtype code c, but the table holds ``want_code``
+  //   want_code: the table's dtype code, or -1 when the table is still empty
+  int append(py::dict params, py::dict index, py::list shapes, py::object weight, int want_code) {
+    const double w = PyFloat_AsDouble(weight.ptr());
+    if (PyErr_Occurred()) {
+      PyErr_Clear();
+      return -1;
+    }
+    if (PyList_GET_SIZE(shapes.ptr()) != T_) return -1;
+    const size_t base = ptrs_.size();
+    ptrs_.resize(base + T_, 0);
+    numels_.resize(base + T_, -1);
+    uint64_t* p = ptrs_.data() + base;
+    int64_t* n = numels_.data() + base;
+    const size_t kbase = keep_.size();
+    int code = -2;
+    Py_ssize_t seen = 0;
+    PyObject *key, *value;
+    Py_ssize_t pos = 0;
+    auto rollback = [&](int rc) {
+      ptrs_.resize(base);
+      numels_.resize(base);
+      keep_.resize(kbase);
+      return rc;
+    };
+    while (PyDict_Next(params.ptr(), &pos, &key, &value)) {
+      PyObject* seg_obj = PyDict_GetItem(index.ptr(), key);  // borrowed
+      if (seg_obj == nullptr) return rollback(-1);           // a name the layout does not know
+      ++seen;
+      const long long seg = PyLong_AsLongLong(seg_obj);
+      if (!THPVariable_Check(value)) return rollback(-1);
+      const at::Tensor& t = THPVariable_Unpack(value);
+      if (seg < 0) {  // a zero-element tensor of the layout: no segment
+        if (t.numel() != 0) return rollback(-1);
+        continue;
+      }
+      if (seg >= T_ || n[seg] >= 0) return rollback(-1);
+      if (!t.is_cuda() || t.get_device() != dev_ || !t.is_contiguous()) return rollback(-1);
+      const int c = dtype_code(t.scalar_type());
+      if (c < 0 || (code != -2 && c != code)) return rollback(-1);
+      code = c;
+      if (!same_shape(t, PyList_GET_ITEM(shapes.ptr(), seg))) return rollback(-1);
+      p[seg] = reinterpret_cast<uint64_t>(t.data_ptr());
+      n[seg] = t.numel();
+      keep_.push_back(t);
+    }
+    if (code < 0) return rollback(-1);
+    if (want_code >= 0 && code != want_code) return rollback(-2 - code);
+    if (esize_ == 0) esize_ = esize_of(code);
+    weights_.resize(base + T_);
+    double* wr = weights_.data() + base;
+    for (int64_t s = 0; s < T_; ++s) wr[s] = n[s] >= 0 ? w : 0.0;
+    ++rows_;
+    const bool complete = seen == PyDict_Size(index.ptr());
+    return code | (complete ? 16 : 0);
+  }
+
+  // append_row(ptrs, weights, numels, esize, keep): a row the caller has checked (the general
+  // staging path, host updates packed by the pinned ingest); numels[s] == -1 marks an absent entry
+  void append_row(py::list ptrs, py::list weights, py::list numels, int64_t esize, py::list keep) {
+    if (PyList_GET_SIZE(ptrs.ptr()) != T_ || PyList_GET_SIZE(weights.ptr()) != T_ ||
+        PyList_GET_SIZE(numels.ptr()) != T_)
+      throw std::invalid_argument("client row does not match the layout");
+    if (esize_ != 0 && esize != esize_) throw std::invalid_argument("a row of another element size");
+    const size_t base = ptrs_.size();
+    std::vector<uint64_t> p(T_);
+    std::vector<double> wr(T_);
+    std::vector<int64_t> nr(T_);
+    for (int64_t s = 0; s < T_; ++s) {
+      p[s] = PyLong_AsUnsignedLongLongMask(PyList_GET_ITEM(ptrs.ptr(), s));
+      wr[s] = PyFloat_AsDouble(PyList_GET_ITEM(weights.ptr(), s));
+      nr[s] = PyLong_AsLongLong(PyList_GET_ITEM(numels.ptr(), s));
+    }
+    if (PyErr_Occurred()) throw py::error_already_set();
+    ptrs_.insert(ptrs_.end(), p.begin(), p.end());
+    weights_.insert(weights_.end(), wr.begin(), wr.end());
+    numels_.insert(numels_.end(), nr.begin(), nr.end());
+    (void)base;
+    for (auto item : keep) extra_keep_.push_back(py::reinterpret_borrow<py::object>(item));
+    esize_ = esize;
+    ++rows_;
+  }
+
+  // validate(numels, esize, device_index): every present entry has numels[s] elements of esize
+  // bytes on the device. Returns "" or a message naming the first bad entry.
+  std::string validate(py::list numels, int64_t esize, int64_t device_index) const {
+    if (PyList_GET_SIZE(numels.ptr()) != T_) return "the layout does not match the table";
+    std::vector<int64_t> want(T_);
+    for (int64_t s = 0; s < T_; ++s) want[s] = PyLong_AsLongLong(PyList_GET_ITEM(numels.ptr(), s));
+    if (rows_ && (esize != esize_ || device_index != dev_))
+      return "rows of " + std::to_string(esize_) + "-byte elements on device " + std::to_string(dev_) +
+             "; the input format needs " + std::to_string(esize) + " bytes on device " + std::to_string(device_index);
+    for (int64_t k = 0; k < rows_; ++k)
+      for (int64_t s = 0; s < T_; ++s) {
+        const int64_t have = numels_[k * T_ + s];
+        if (have >= 0 && have != want[s])
+          return "client " + std::to_string(k) + ", tensor " + std::to_string(s) + ": " + std::to_string(have) +
+                 " elements; the layout needs " + std::to_string(want[s]);
+      }
+    return "";
+  }
+
+  py::bytes ptr_bytes() const {
+    return py::bytes(reinterpret_cast<const char*>(ptrs_.data()), ptrs_.size() * sizeof(uint64_t));
+  }
+  py::bytes weight_bytes() const {
+    return py::bytes(reinterpret_cast<const char*>(weights_.data()), weights_.size() * sizeof(double));
+  }
+  py::bytes numel_bytes() const {
+    return py::bytes(reinterpret_cast<const char*>(numels_.data()), numels_.size() * sizeof(int64_t));
+  }
+  int64_t num_clients() const { return rows_; }
+  int64_t num_segments() const { return T_; }
+  int64_t esize() const { return esize_; }
+
+ private:
+  static int64_t esize_of(int code) { return code == 3 ? 8 : (code == 0 ? 4 : 2); }
+  int64_t T_, dev_;
+  int64_t rows_ = 0, esize_ = 0;
+  std::vector<uint64_t> ptrs_;
+  std::vector<double> weights_;
+  std::vector<int64_t> numels_;
+  std::vector<at::Tensor> keep_;      // the staged tensors stay alive until the table is dropped
+  std::vector<py::object> extra_keep_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "host-side staging of plugin updates (see staging_ext.cpp)";
+  py::class_<Rows>(m, "Rows")
+      .def(py::init<int64_t, int64_t>())
+      .def("append", &Rows::append)
+      .def("append_row", &Rows::append_row)
+      .def("validate", &Rows::validate)
+      .def("ptr_bytes", &Rows::ptr_bytes)
+      .def("weight_bytes", &Rows::weight_bytes)
+      .def("numel_bytes", &Rows::numel_bytes)
+      .def_property_readonly("num_clients", &Rows::num_clients)
+      .def_property_readonly("num_segments", &Rows::num_segments)
+      .def_property_readonly("esize", &Rows::esize);
   m.def("stage_resident", &stage_resident);
   m.def("resident_row", &resident_row);
   m.def("row_pointers", &row_pointers);

@@ -273,6 +273,24 @@ class OutputTable:
         self.device = device
         self.c_array = (ctypes.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
 
+    @classmethod
+    def from_flat(cls, flat: torch.Tensor, offsets: Sequence[int], layout: ModelLayout) -> OutputTable:
+        """Segments of one flat contiguous buffer at element ``offsets`` (no tensor per segment:
+        the pointer array is computed from the buffer's address)."""
+        if flat.dim() != 1 or not flat.is_contiguous() or len(offsets) != layout.num_segments:
+            raise ValueError("a flat contiguous buffer and one offset per segment are required")
+        offs = np.asarray(offsets, dtype=np.int64)
+        if layout.num_segments and (offs.min() < 0 or int((offs + np.asarray(layout.numels)).max()) > flat.numel()):
+            raise ValueError("segment outside the flat output buffer")
+        self = cls.__new__(cls)
+        self.tensors = [flat]
+        self.dtype = flat.dtype
+        self.layout = layout
+        self.device = flat.device
+        ptrs = np.uint64(flat.data_ptr()) + offs.astype(np.uint64) * np.uint64(flat.element_size())
+        self.c_array = (ctypes.c_void_p * layout.num_segments).from_buffer_copy(ptrs.tobytes())
+        return self
+
 
 class FedAvgContext:
     """One native FedAvg context: layout + device + fp64 accumulator."""

@@ -135,6 +135,21 @@ def is_delta_message(obj: Any) -> bool:
     return "delta_parameter" in _field_names(obj) and is_parameter_message_base(obj)
 
 
+KIND_OTHER, KIND_PARAMETER, KIND_DELTA = 0, 1, 2
+_KIND_CACHE: dict[type, int] = {}
+
+
+def message_kind(obj: Any) -> int:
+    """KIND_PARAMETER / KIND_DELTA / KIND_OTHER of ``obj`` (is_parameter_message /
+    is_delta_message in one class-keyed lookup: the plugins ask once per arrival)."""
+    cls = type(obj)
+    kind = _KIND_CACHE.get(cls)
+    if kind is None:
+        kind = KIND_PARAMETER if is_parameter_message(obj) else KIND_DELTA if is_delta_message(obj) else KIND_OTHER
+        _KIND_CACHE[cls] = kind
+    return kind
+
+
 def wire_class(like: Any, name: str) -> type:
     """The class ``name`` ("ParameterMessage", "MultipleWorkerMessage", ...) of the wire module
     ``like`` comes from; this package's class when ``like`` is None or its module has none."""

@@ -52,8 +52,9 @@ from .fedavg import ClientTable, FedAvgContext, NaNAggregationError, OutputTable
 EXCHANGES = ("auto", "reduce", "scatter")
 # chunk shapes: equal ranges; the last chunk half the others (a short exchange tail when the
 # exchange keeps up with the fold); the first chunk half the others (the exchange starts sooner
-# when it does not)
-CHUNK_SHAPES = ("even", "taper", "ramp")
+# when it does not); the last chunk a quarter of the others (a shorter tail still, for links
+# fast enough to keep up with three full chunks)
+CHUNK_SHAPES = ("even", "taper", "ramp", "tail")
 
 
 FLAG_BITS = 16  # NaN flag words are bit sets: FLAG_ACC_NAN / RESULT / CENTRAL, local-error bits above
@@ -312,6 +313,9 @@ def chunk_edges(num_tiles: int, chunks: int, shape: str = "even") -> list[int]:
     chunks = max(1, min(chunks, num_tiles))
     if shape == "even" or chunks == 1:
         weights = [1.0] * chunks
+    elif shape == "tail":
+        weights = [4.0] * chunks
+        weights[-1] = 1.0
     else:
         weights = [2.0] * chunks
         weights[-1 if shape == "taper" else 0] = 1.0
@@ -328,6 +332,100 @@ def chunk_edges(num_tiles: int, chunks: int, shape: str = "even") -> list[int]:
 def chunk_bounds(num_tiles: int, chunks: int, shape: str = "even") -> list[tuple[int, int]]:
     edges = chunk_edges(num_tiles, chunks, shape)
     return [(edges[i], edges[i + 1]) for i in range(len(edges) - 1)]
+
+
+class ExchangeModel:
+    """Per-round cost model of the client-sharded reduce: G ranks, each folding
+    its shard into an fp64 partial in tile chunks, the exchange of chunk c on the comm stream
+    behind the fold of chunk c, the root's division of every chunk but the last overlapped with
+    the last exchange (``fedavg_sharded_round``), the last chunk's exchange and division exposed.
+
+    The rates: ``fold_rate`` and ``hbm_rate`` are measured on one MI355X (the partial kernel's
+    6.45 TB/s over a 256 x ResNet-18 shard, profiles/r02_sharded_and_anchor.jsonl; the finalize is
+    an HBM stream at the same rate); ``link_rate`` is the quoted xGMI rate per link and direction
+    (7 links per GPU, one per peer) and ``link_eff`` the share of it RCCL is assumed to reach —
+    neither is measurable on the one-GPU boxes this build is tested on, so the tuner
+    (``tune_exchange``) has the last word on a node. ``underfill_ms``: a chunk of fewer than
+    ``full_chunk_tiles`` 4096-element tiles leaves CUs idle at its end (measured: 8 chunks of
+    357 tiles +0.07 ms per one-rank round against 2-4 chunks)."""
+
+    def __init__(self, fold_rate: float = 6.45e12, hbm_rate: float = 6.5e12, link_rate: float = 153e9,
+                 link_eff: float = 0.75, full_chunk_tiles: int = 512, underfill_ms: float = 0.009) -> None:
+        self.fold_rate, self.hbm_rate = fold_rate, hbm_rate
+        self.link_rate, self.link_eff = link_rate, link_eff
+        self.full_chunk_tiles, self.underfill_ms = full_chunk_tiles, underfill_ms
+
+    def one_gpu_ms(self, numel: int, n_clients: int, in_bytes: int, out_bytes: int) -> float:
+        """The fused single-launch round on one GPU (the strong-scaling anchor)."""
+        return (n_clients * numel * in_bytes + numel * out_bytes) / self.fold_rate * 1e3
+
+    def round_ms(self, world: int, numel: int, n_clients: int, in_bytes: int, out_bytes: int,
+                 edges: Sequence[int], exchange: str, root_clients: int | None = None) -> dict[str, float]:
+        """Predicted terms of one round. Every rank's HBM carries its fold (its clients + the fp64
+        partial write) and its share of the exchange (RCCL reads the partial and writes the
+        received sums: ~2 x the chunk per rank); the root's also the division. The exchange of
+        chunk c starts once every rank has folded chunk c and the previous exchange is done; it
+        is link-bound. ``root_clients``: the root's shard (default: an even split), the others
+        share the rest — a smaller root shard leaves HBM time for the root's division."""
+        G = world
+        n_root = -(-n_clients // G) if root_clients is None else root_clients
+        n_peer = -(-(n_clients - n_root) // (G - 1)) if G > 1 else 0
+        link = self.link_rate * self.link_eff
+        rate = self.fold_rate / 1e3  # bytes per ms
+        part_b, res_b = numel * 8, numel * out_bytes
+        total_tiles = edges[-1]
+        fracs = [(b - a) / total_tiles for a, b in zip(edges, edges[1:])]
+        under = [self.underfill_ms if b - a < self.full_chunk_tiles else 0.0 for a, b in zip(edges, edges[1:])]
+        root_t = peer_t = x_end = 0.0
+        xs, x_ends = [], []
+        for c, f in enumerate(fracs):
+            # the exchange of the previous chunk shares HBM with this chunk's fold on every rank
+            xh = 2 * fracs[c - 1] * part_b if c else 0.0
+            root_t += (f * (n_root * numel * in_bytes + part_b) + xh) / rate + under[c]
+            peer_t += (f * (n_peer * numel * in_bytes + part_b) + xh) / rate + under[c]
+            ready = max(root_t, peer_t if G > 1 else 0.0)
+            if exchange == "reduce":
+                x = f * part_b / ((G - 1) * link) * 1e3  # the root takes the partial over G - 1 links
+            else:  # reduce-scatter out of / into every rank over G - 1 links, then the result gather
+                x = (f * part_b / G + f * res_b / G) / link * 1e3 + f * (part_b + res_b) / G / rate
+            x_end = max(x_end, ready) + x
+            xs.append(x)
+            x_ends.append(x_end)
+        last = fracs[-1]
+        if exchange == "reduce":
+            # the root divides the head chunks once they are reduced, during the last exchange
+            head_div = (1 - last) * (part_b + res_b) / rate if len(fracs) > 1 else 0.0
+            head_end = max(root_t, x_ends[-2]) + head_div if len(fracs) > 1 else 0.0
+            last_div = last * (part_b + res_b) / rate
+            step = max(x_end, head_end) + last_div
+        else:
+            last_div = 2 * res_b / rate  # the root's copy-out of the gathered result
+            step = x_end + last_div
+        fold = max(root_t, peer_t if G > 1 else 0.0)
+        t1 = self.one_gpu_ms(numel, n_clients, in_bytes, out_bytes)
+        return {"fold_ms": round(fold, 4), "exposed_exchange_and_finalize_ms": round(step - fold, 4),
+                "last_chunk_exchange_ms": round(xs[-1], 4), "last_finalize_ms": round(last_div, 4),
+                "root_clients": n_root, "peer_clients": n_peer,
+                "step_ms": round(step, 4), "one_gpu_ms": round(t1, 4), "speedup": round(t1 / step, 3)}
+
+    def best(self, world: int, numel: int, n_clients: int, in_bytes: int, out_bytes: int, num_tiles: int,
+             candidates: Sequence[tuple[str, int, str]] | None = None,
+             balance_root: bool = True) -> tuple[tuple[str, int, str], dict]:
+        """The candidate (exchange, chunks, shape) — and, with ``balance_root``, the root's shard
+        (an even split or up to 8 clients fewer) — with the smallest predicted step."""
+        cands = list(candidates) if candidates is not None else exchange_candidates()
+        even = -(-n_clients // world)
+        roots = range(max(1, even - 8), even + 1) if balance_root and world > 1 else [even]
+        best = None
+        for i, (ex, ch, sh) in enumerate(cands):
+            edges = chunk_edges(num_tiles, ch, sh)
+            for nr in roots:
+                r = self.round_ms(world, numel, n_clients, in_bytes, out_bytes, edges, ex, nr)
+                key = (r["step_ms"], -nr, i)
+                if best is None or key < best[0]:
+                    best = (key, cands[i], r)
+        assert best is not None
+        return best[1], best[2]
 
 
 def sharded_reduce(
@@ -400,11 +498,11 @@ def sharded_reduce(
 
 
 def exchange_candidates(chunks: int | None = None, shapes: Sequence[str] = CHUNK_SHAPES) -> list[tuple[str, int, str]]:
-    """(exchange, chunks, shape) triples ``tune_exchange`` tries: both exchanges at 2 / 4 / 8
+    """(exchange, chunks, shape) triples ``tune_exchange`` tries: both exchanges at 2 / 4 / 6 / 8
     chunks (or the given count only), every chunk shape (one shape when there is one chunk)."""
     out = []
     for ex in ("reduce", "scatter"):
-        for c in ((chunks,) if chunks else (2, 4, 8)):
+        for c in ((chunks,) if chunks else (2, 4, 6, 8)):
             for sh in (shapes if c > 1 else ("even",)):
                 out.append((ex, c, sh))
     return out
@@ -493,10 +591,20 @@ def _reduce_exchange(reducer: LocalReducer, global_totals: list[float], bounds: 
     # The collectives of one process group run on one RCCL stream and complete in issue
     # order, so on the GPU one wait (the last reduce) covers every chunk: one cross-stream
     # dependency instead of one per chunk. Host backends (gloo) wait for each work.
+    if rank == root:
+        reducer.set_accumulated(global_totals)
+    if acc.is_cuda and len(works) >= 2 and rank == root:
+        # the chunks already reduced are divided while the last one is still being reduced
+        # (fedavg_sharded_round does the same): only the last chunk's division
+        # follows the last collective
+        works[-2].wait()
+        reducer.finalize_range(0, bounds[-1][0])
+        works[-1].wait()
+        reducer.finalize_range(bounds[-1][0], reducer.num_tiles)
+        return
     for w in (works[-1:] if acc.is_cuda else works):
         w.wait()
     if rank == root:
-        reducer.set_accumulated(global_totals)
         reducer.finalize_range(0, reducer.num_tiles)  # one launch over every tile
 
 

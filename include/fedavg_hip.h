@@ -102,6 +102,17 @@ int32_t fedavg_abi_version(void);
 #define FEDAVG_BUILD_ABLATE_QSGD 0x2
 int32_t fedavg_build_flags(void);
 
+/* A compile-time constant of the kernels' geometry, by name, into *out (test support: the
+ * property tests place their sizes around every edge the kernels have, derived from the build
+ * instead of copied into the tests). Names: "tile", "tile_wide", "split_tile"; per input dtype
+ * d in {f32, f16, bf16, f64}: "ae_<d>", "lanes_<d>" (elements per lane / lanes per tile of the
+ * whole-layout table), "ae4096_<d>", "lanes4096_<d>" (the 4096-element table), "group_<d>"
+ * (clients loaded per group), "pipe_<d>" (clients per pipeline stage, 0 = no pipeline);
+ * "qsgd_tile", "qsgd_ae", "qsgd_group"; "pers_chunk", "pers_jb" (receivers per wave),
+ * "pers_group" (receivers per launch), "pers_u", "pers_ring_stage", "pers_ring_depth".
+ * FEDAVG_ERR_INVALID for an unknown name. */
+int32_t fedavg_kernel_constant(const char* name, int64_t* out);
+
 /* Byte size of one QSGD record of a numel-element tensor, and the offset of its sign bits
  * (see FEDAVG_QSGD_F32). Pure functions; -1 for numel < 0. */
 int64_t fedavg_qsgd_record_bytes(int64_t numel);

@@ -106,3 +106,46 @@ def test_native_host_staging_bit_identical(hip_device, wave, dtype):
     assert list(got) == list(want)
     for n, v in want.items():
         assert bits_equal(got[n].cpu().numpy(), v), n
+
+
+@pytest.mark.parametrize("wave", [2, 64])
+def test_uniform_totals_then_partial_and_late_updates(hip_device, wave):
+    # complete updates keep one running total for every name; a partial update (a missing key)
+    # and a late key (a name first seen mid-round) write it out per name first. Float weights make
+    # every total order-sensitive; two rounds on one object check that the state is reset.
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=wave)
+    g = torch.Generator().manual_seed(17)
+    rng = np.random.default_rng(17)
+    for rnd in range(2):
+        oracle = OracleFedAvg()
+        for k in range(8):
+            shapes = dict(SHAPES)
+            if k == 4:
+                del shapes["fc"]
+            if k == 6 and rnd == 0:
+                shapes["late"] = (7,)
+            p = {n: torch.randn(s, generator=g) for n, s in shapes.items()}
+            w = float(rng.uniform(0.1, 3.0)) if k % 3 else int(rng.integers(1, 9))
+            algo.process_worker_data(k, ParameterMessage(parameter={n: t.to(hip_device) for n, t in p.items()},
+                                                         aggregation_weight=w))
+            oracle.process_worker_data(k, OracleMessage(parameter={n: t.numpy() for n, t in p.items()},
+                                                        aggregation_weight=w))
+        got = algo.aggregate_worker_data().parameter
+        want = oracle.aggregate_worker_data().parameter
+        assert list(got) == list(want), rnd
+        for n, v in want.items():
+            assert bits_equal(got[n].cpu().numpy(), v), (rnd, n)
+        algo.clear_worker_data()
+
+
+def test_common_arrivals_take_the_native_table(hip_device):
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=64)
+    for k in range(3):
+        p = {n: torch.ones(s, device=hip_device) for n, s in SHAPES.items()}
+        algo.process_worker_data(k, ParameterMessage(parameter=p, aggregation_weight=k + 1))
+    table = algo._FedAVGAlgorithm__table
+    assert isinstance(table, _staging.NativeClientTable) and table.num_clients == 3
+    # one running total for every name while every update is complete
+    assert algo._FedAVGAlgorithm__uniform_count == 3 and algo._FedAVGAlgorithm__host_totals == {}
+    out = algo.aggregate_worker_data().parameter
+    assert float(out["conv"].flatten()[0]) == 1.0

@@ -18,7 +18,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from distributed_learning_simulation_lib_amd.fedavg import ModelLayout
-from distributed_learning_simulation_lib_amd.sharded import chunk_bounds, sharded_reduce
+from distributed_learning_simulation_lib_amd.sharded import chunk_bounds, exchange_candidates, sharded_reduce
 from oracle.fedavg_oracle import fedavg_flat
 from tests.helpers import rendezvous_url
 
@@ -282,7 +282,6 @@ def test_tune_exchange_agrees_across_ranks():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from distributed_learning_simulation_lib_amd.sharded import exchange_candidates
 
     assert got[0][0] == got[1][0]  # max-over-ranks times: one answer everywhere
     assert got[0][1] == sorted(exchange_candidates()) and got[0][0] in exchange_candidates()
@@ -295,12 +294,12 @@ def test_tune_exchange_agrees_across_ranks():
 
 
 def test_exchange_candidates():
-    from distributed_learning_simulation_lib_amd.sharded import exchange_candidates
 
     assert exchange_candidates(4) == [("reduce", 4, "even"), ("reduce", 4, "taper"), ("reduce", 4, "ramp"),
-                                      ("scatter", 4, "even"), ("scatter", 4, "taper"), ("scatter", 4, "ramp")]
+                                      ("reduce", 4, "tail"), ("scatter", 4, "even"), ("scatter", 4, "taper"),
+                                      ("scatter", 4, "ramp"), ("scatter", 4, "tail")]
     assert exchange_candidates(1) == [("reduce", 1, "even"), ("scatter", 1, "even")]
-    assert len(exchange_candidates()) == 18
+    assert len(exchange_candidates()) == 32
 
 
 def test_resolve_exchange():
@@ -330,6 +329,7 @@ def test_chunk_shapes():
     assert chunk_edges(1427, 4) == [0, 357, 714, 1070, 1427]
     taper, ramp = chunk_edges(1400, 4, "taper"), chunk_edges(1400, 4, "ramp")
     assert taper == [0, 400, 800, 1200, 1400] and ramp == [0, 200, 600, 1000, 1400]
+    assert chunk_edges(1300, 4, "tail") == [0, 400, 800, 1200, 1300]
     assert chunk_edges(10, 1, "taper") == [0, 10]
     with pytest.raises(ValueError):
         chunk_edges(10, 2, "zigzag")
@@ -386,3 +386,23 @@ def test_rccl_comm_ships_rank0_id_to_every_rank():
         assert p.exitcode == 0
     for rank, joined, w, r in got:
         assert joined == (_FakeCommLib.ID, world, rank) and (w, r) == (world, rank)
+
+
+def test_exchange_model_terms():
+    """DESIGN.md §5 cost model: the anchor, the pipeline and the choice it makes for config 3."""
+    from distributed_learning_simulation_lib_amd.sharded import ExchangeModel, chunk_edges
+
+    m = ExchangeModel()
+    P, tiles = 11_689_512, 2854  # ResNet-18, 4096-element tiles
+    assert abs(m.one_gpu_ms(P, 256, 4, 4) - 1.863) < 0.01  # the measured 1.864 ms anchor
+    for G in (2, 4, 8):
+        (ex, ch, sh), r = m.best(G, P, 256, 4, 4, tiles)
+        assert (ex, ch, sh) in exchange_candidates()
+        assert r["step_ms"] >= r["fold_ms"] > 0 and r["speedup"] < G
+        # nothing beats the fold: the even 4-chunk reduce costs at least as much as the choice
+        even = m.round_ms(G, P, 256, 4, 4, chunk_edges(tiles, 4, "even"), "reduce")
+        assert even["step_ms"] >= r["step_ms"]
+    # a faster link shortens the exposed tail, a slower one lengthens it
+    fast, slow = ExchangeModel(link_eff=1.0), ExchangeModel(link_eff=0.4)
+    e = chunk_edges(tiles, 4, "taper")
+    assert fast.round_ms(4, P, 256, 4, 4, e, "reduce")["step_ms"] < slow.round_ms(4, P, 256, 4, 4, e, "reduce")["step_ms"]

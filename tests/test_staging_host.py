@@ -41,3 +41,36 @@ def test_views_of_a_flat_buffer():
     assert flat[8] == -1.0
     with pytest.raises(IndexError):
         ext.views(flat, [38], [(4,)])  # outside the buffer
+
+
+def test_native_rows_refuse_host_updates_unchanged():
+    rows = ext.Rows(2, 0)
+    params = {"a": torch.ones(3), "b": torch.ones(2, 2)}
+    assert rows.append(params, {"a": 0, "b": 1}, [(3,), (2, 2)], 2.0, -1) == -1
+    assert rows.append({"z": torch.ones(1)}, {"a": 0, "b": 1}, [(3,), (2, 2)], 2.0, -1) == -1
+    assert rows.append(params, {"a": 0, "b": 1}, [(3,), (2, 2)], object(), -1) == -1
+    assert rows.num_clients == 0 and rows.ptr_bytes() == b""
+
+
+def test_native_rows_general_appends_and_validation():
+    import numpy as np
+
+    t = _staging.NativeClientTable(3, 0)
+    t.add_resident_client([16, 0, 48], [2.0, 0.0, 2.0], [5, -1, 7], 4, 0, [])
+    t.add_resident_client([64, 80, 96], [3, 3, 3], [5, 6, 7], 4, 0, [])
+    assert t.num_clients == 2
+    p, w = t.arrays()
+    assert p.tolist() == [16, 0, 48, 64, 80, 96] and w.tolist() == [2.0, 0.0, 2.0, 3.0, 3.0, 3.0]
+    assert np.frombuffer(t.rows.numel_bytes(), dtype=np.int64).tolist() == [5, -1, 7, 5, 6, 7]
+    t.validate([5, 6, 7], 4, 0, "k")  # absent entries are skipped
+    with pytest.raises(ValueError, match="client 0, tensor 2: 7 elements; the layout needs 8"):
+        t.validate([5, 6, 8], 4, 0, "k2")
+    with pytest.raises(ValueError, match="input format needs 2 bytes"):
+        t.validate([5, 6, 7], 2, 0, "k3")
+    with pytest.raises(ValueError, match="device"):
+        t.add_resident_client([1, 2, 3], [1, 1, 1], [5, 6, 7], 4, 1, [])
+    with pytest.raises(ValueError):
+        t.add_resident_client([1, 2], [1, 1], [5, 6], 4, 0, [])  # not a full row
+    with pytest.raises(ValueError):
+        t.add_resident_client([1, 2, 3], [1, 1, 1], [5, 6, 7], 8, 0, [])  # another element size
+    assert t.num_clients == 2

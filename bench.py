@@ -291,7 +291,7 @@ def hbm_probes(device: torch.device, nbytes: int = 4 << 30) -> dict:
     return out
 
 
-def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3) -> dict:
+def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dtype: torch.dtype = torch.float32) -> dict:
     """The reference's CPU path on the host cores, rank 0, N=1: the reference's
     FedAVGAlgorithm call sequence (oracle/ref_torch_cpu.py: process_worker_data per client with
     its torch CPU ops, then aggregate_worker_data) over ``n_clients`` pre-built messages of the
@@ -306,8 +306,9 @@ def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3) -> 
     clients = []
     for i in range(n_clients):  # generation is outside the timed region
         g = torch.Generator().manual_seed(1234 + i)
-        clients.append({n: torch.randn(s, generator=g, dtype=torch.float32) for n, s in zip(layout.names, layout.shapes)})
-    nbytes = n_clients * layout.total_numel * 4 + layout.total_numel * 4
+        clients.append({n: torch.randn(s, generator=g, dtype=torch.float32).to(dtype)
+                        for n, s in zip(layout.names, layout.shapes)})
+    nbytes = n_clients * layout.total_numel * dtype.itemsize + layout.total_numel * 4
     times = []
     t_start = time.perf_counter()
     for _ in range(repeats):
@@ -327,8 +328,8 @@ def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3) -> 
         "kind": "port",
         "seconds_per_round": round(best, 4),
         "sample": (
-            f"the full headline round: {n_clients} pre-built ParameterMessages x {layout.num_segments}-tensor layout "
-            f"({layout.total_numel:,} fp32 params), the reference's FedAVGAlgorithm call sequence "
+            f"the full round: {n_clients} pre-built ParameterMessages x {layout.num_segments}-tensor layout "
+            f"({layout.total_numel:,} {str(dtype).split('.')[-1]} params), the reference's FedAVGAlgorithm call sequence "
             f"(process_worker_data x {n_clients}: isnan, to(f64)*w, +=; aggregate_worker_data: isnan, /W, isnan) "
             f"in torch CPU ops, best of {repeats} ({time.perf_counter() - t_start:.1f} s)"
         ),
@@ -647,8 +648,13 @@ def main_plugin(args: argparse.Namespace) -> int:
     wave = args.wave if args.wave > 0 else N
     algo = FedAVGAlgorithm(device=device, wave_size=wave, result_dtype=out_dtype)
 
+    # --workload gradient: GradientWorker._process_gradient's message every step (gradient_worker.py:
+    # 83-93): the native-dtype gradient dict, in_round=True, the dataset size as weight
+    in_round = args.workload == "gradient"
+
     def messages() -> list:
-        return [ParameterMessage(parameter=dict(p), aggregation_weight=w) for p, w in zip(params, weights)]
+        return [ParameterMessage(parameter=dict(p), aggregation_weight=w, in_round=in_round)
+                for p, w in zip(params, weights)]
 
     host_s = [0.0]
 
@@ -659,7 +665,7 @@ def main_plugin(args: argparse.Namespace) -> int:
         host_s[0] += time.perf_counter() - h0
         res = algo.aggregate_worker_data()  # ends on the host: the NaN flags are read (:93, :97)
         algo.clear_worker_data()
-        assert len(res.parameter) == T
+        assert len(res.parameter) == T and res.in_round == in_round
 
     for _ in range(args.warmup):
         step()
@@ -687,21 +693,32 @@ def main_plugin(args: argparse.Namespace) -> int:
         del params, views, buckets
         algo.exit()
         torch.cuda.empty_cache()
-        cpu = cpu_baseline(layout)
+        cpu = cpu_baseline(layout, n_clients=N, dtype=in_dtype)
+        if in_round:  # the same round, as a latency
+            cpu = dict(cpu, value=round(cpu["seconds_per_round"] * 1e3, 3), unit="ms per round")
     short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
+    gbps = round(job_bytes / step_s / 1e9, 2)
     line = {
-        "metric": "aggregated GB/s (device-resident) through the plugin surface: FedAVGAlgorithm."
-                  "process_worker_data x N + aggregate_worker_data",
-        "value": round(job_bytes / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
-        "scaling": "replicas only", "vs_baseline": None, "dtype": "f64",
+        "metric": ("in-round gradient FedAvg round latency (GradientWorker cadence) through the plugin surface: "
+                   "FedAVGAlgorithm.process_worker_data x N + aggregate_worker_data" if in_round else
+                   "aggregated GB/s (device-resident) through the plugin surface: FedAVGAlgorithm."
+                   "process_worker_data x N + aggregate_worker_data"),
+        "value": round(step_s * 1e3, 4) if in_round else gbps, "unit": "ms per round" if in_round else "GB/s",
+        "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": not in_round,
+        "scaling": "replicas only", "vs_baseline": None, "dtype": "f64", "GBps": gbps,
         "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
-        "config": {"workload": f"plugin_fedavg_{args.layout}_{short}_{N}_clients" + (f"_waves_of_{wave}" if n_waves > 1 else ""),
+        "config": {"workload": (f"{'gradient' if in_round else 'plugin'}_fedavg_{args.layout}_{short}_{N}_clients"
+                                + (f"_waves_of_{wave}" if n_waves > 1 else "")),
                    "clients": N, "params_per_client": P, "tensors_per_client": T, "in_dtype": args.in_dtype,
-                   "out_dtype": args.out_dtype, "clients_per_launch": wave,
+                   "out_dtype": args.out_dtype, "clients_per_launch": wave, "in_round": in_round,
                    "host_us_per_update": round(host_s[0] / (args.steps * N) * 1e6, 2),
                    "process_worker_data_ms_per_round": round(host_s[0] / args.steps * 1e3, 4),
-                   "baseline_config": "BASELINE.json configs[1] through the reference's plugin call sequence"},
+                   # what a round costs beyond its kernels: staging, launch, NaN readback, result dict
+                   "fixed_ms_per_round": round((step_s - kstep_s) * 1e3, 4),
+                   "baseline_config": ("GradientWorker in-round rounds (gradient_worker.py:83-93), see DESIGN.md §4"
+                                       if in_round else
+                                       "BASELINE.json configs[1] through the reference's plugin call sequence")},
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
@@ -918,7 +935,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layout", default="resnet18", choices=sorted(LAYOUTS))
-    ap.add_argument("--clients-per-gpu", type=int, default=64,
+    ap.add_argument("--clients-per-gpu", type=int, default=None,
                     help="weak scaling (--weak) and the personalized / qsgd workloads: clients per GPU")
     ap.add_argument("--total-clients", type=int, default=0,
                     help="clients of the whole job, sharded over the ranks (0 = auto: --clients-per-gpu "
@@ -956,10 +973,12 @@ def main() -> int:
     ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
-    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd", "plugin"],
+    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd", "plugin", "gradient"],
                     help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU); "
                          "qsgd: FedAvg over QSGD-quantised updates, dequantisation fused (one GPU); "
-                         "plugin: the headline round through FedAVGAlgorithm's plugin calls (one GPU)")
+                         "plugin: the headline round through FedAVGAlgorithm's plugin calls (one GPU); "
+                         "gradient: GradientWorker's in-round rounds through the plugin, as a latency "
+                         "(--clients-per-gpu default 8)")
     ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
     ap.add_argument("--launch-timeout", type=float, default=1200.0,
                     help="--gpus N > 1 without an external launcher: seconds before the spawned ranks are "
@@ -970,14 +989,16 @@ def main() -> int:
                          "with value null (no measurement)")
     args = ap.parse_args()
     if args.out_dtype is None:
-        args.out_dtype = "float64" if args.workload == "plugin" else "float32"
+        args.out_dtype = "float64" if args.workload in ("plugin", "gradient") else "float32"
+    if args.clients_per_gpu is None:
+        args.clients_per_gpu = 8 if args.workload == "gradient" else 64
     if args.dry_run:
         return main_dry(args)
     if args.workload == "personalized":
         return main_personalized(args)
     if args.workload == "qsgd":
         return main_qsgd(args)
-    if args.workload == "plugin":
+    if args.workload in ("plugin", "gradient"):
         return main_plugin(args)
     if args.shard == "elements":
         return main_elements(args)

@@ -139,6 +139,9 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_BALANCE_DEFAULT  // balanced whole-layout tile orders (bit 0 fp32, bit 1 fp64); env FEDAVG_BALANCE
 #define FEDAVG_BALANCE_DEFAULT 3
 #endif
+#ifndef FEDAVG_PARTV  // 1 = tiles of whole lane-vectors take the grouped fast path (A/B knob; pair 0 with
+#define FEDAVG_PARTV 1  // FEDAVG_BALANCE_DEFAULT=0, whose pieces are such tiles)
+#endif
 #ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
 #define FEDAVG_ACC_NT_LOAD 0
 #endif
@@ -197,6 +200,7 @@ struct KArgs {
   int32_t zero_init;   // start every segment at the identity -0.0, ignore acc_in (shard partials)
   int32_t walk_back;   // the first walk_back tiles of the launch are walked last to first
                        // (fedavg_ctx::walk_reverse); 0 = natural order
+  const double* qtab;  // QSGD: [T][K][256] |product| tables of the call (qsgd_table_kernel)
 };
 
 enum OutKind : int { OUT_ACC = 0, OUT_F32 = 1, OUT_F64 = 2 };
@@ -811,9 +815,10 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
       tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN>(a, td, lds);
     } else {
       bool partv = false;
-      if constexpr (SPLIT == 1 && VEC && LV < TILE) partv = (td.count % LV) == 0;
+      if constexpr (SPLIT == 1 && VEC && LV < TILE && FEDAVG_PARTV) partv = (td.count % LV) == 0;
       if (partv) {
-        if constexpr (SPLIT == 1 && VEC && LV < TILE) tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN, true>(a, td, lds);
+        if constexpr (SPLIT == 1 && VEC && LV < TILE && FEDAVG_PARTV)
+          tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN, true>(a, td, lds);
       } else {
         tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN>(a, td, lds);
       }
@@ -860,57 +865,46 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
 #define FEDAVG_QSGD_GROUP 4
 #endif
 constexpr int kQsgdGroup = FEDAVG_QSGD_GROUP;
+static_assert(FEDAVG_QSGD_GROUP == 4, "one wave of the 256-lane workgroup DMAs each client table of a group");
 constexpr int kQsgdTable = 256;  // entries per client (|p| per slot value)
 constexpr int kQsgdLanes = 256;
 constexpr int kQsgdAE = 16;
 
-// RN(1/level) for the codec levels 1..255 in both codec dtypes (constant-folded: IEEE division),
-// the reciprocal of the table build's division (exact_div.h: the correction step makes the
-// quotient correctly rounded, so each table entry keeps the reference's bits).
-struct QsgdRcp {
-  float f[256];
-  double d[256];
-};
-constexpr QsgdRcp make_qsgd_rcp() {
-  QsgdRcp t{};
-  for (int i = 1; i < 256; ++i) {
-    t.f[i] = 1.0f / static_cast<float>(i);
-    t.d[i] = 1.0 / static_cast<double>(i);
-  }
-  return t;
-}
-__constant__ QsgdRcp kQsgdRcp = make_qsgd_rcp();
-
-__device__ __forceinline__ float fma_dq(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double fma_dq(double a, double b, double c) { return __builtin_fma(a, b, c); }
-
-template <typename DQ>
-__device__ __forceinline__ DQ qsgd_div_level(DQ a, int level) {
-#if FEDAVG_FAST_DIV
-  const DQ L = static_cast<DQ>(level);
-  constexpr DQ kLo = sizeof(DQ) == 4 ? 0x1p-100f : 0x1p-900;
-  constexpr DQ kHi = sizeof(DQ) == 4 ? 0x1p100f : 0x1p900;
-  const DQ m = __builtin_fabs(a);
-  if (__builtin_expect(level >= 1 && level <= 255 && m <= kHi && (m >= kLo || a == DQ(0)), 1)) {
-    const DQ y = sizeof(DQ) == 4 ? static_cast<DQ>(kQsgdRcp.f[level]) : static_cast<DQ>(kQsgdRcp.d[level]);
-    const DQ q0 = a * y;
-    const DQ t = fma_dq(q0, L, -a);  // exact residual, negated (keeps the sign of 0 / L)
-    return fma_dq(-t, y, q0);
-  }
-  return a / L;  // lanes outside the proven range (exec-masked: skipped when no lane needs it)
-#else
-  return a / static_cast<DQ>(level);
-#endif
-}
-
 template <typename DQ>
 __device__ __forceinline__ double qsgd_product(double norm, int level, int slot, double w) {
   // torch evaluates `norm * sign * slot / level` left to right in the codec's dtype; with
-  // sign = +1 the first product is exact, so the non-negative value is (norm * slot) / level.
+  // sign = +1 the first product is exact, so the non-negative value is (norm * slot) / level
+  // (IEEE division, as the codec does it).
   const DQ n = static_cast<DQ>(norm);
-  const DQ v = qsgd_div_level<DQ>(n * static_cast<DQ>(slot), level);
+  const DQ v = (n * static_cast<DQ>(slot)) / static_cast<DQ>(level);
   const double x = static_cast<double>(v);  // .to(float64), fed_avg_algorithm.py:54
   return x * w;
+}
+
+// The |product| tables of one call, built once per (client, tensor) instead of once per tile:
+// table[seg][k][s] = |round(f64(x_hat(s)) * w)| for slot value s of client k's record of segment
+// seg (the sign is applied per element in the fold). One 256-lane workgroup per (client, segment)
+// of the segments [seg_begin, seg_begin + gridDim.y); 2 KiB per table, L2 / MALL resident for
+// the tile kernel's LDS-DMA loads.
+template <typename DQ>
+__global__ __launch_bounds__(kQsgdTable) void qsgd_table_kernel(CallTables tab, int32_t K, int32_t seg_begin,
+                                                                double* qtab) {
+  const int seg = seg_begin + static_cast<int>(blockIdx.y);
+  const int k = static_cast<int>(blockIdx.x);
+  if (k >= to_const<int32_t>(tab.kseg)[seg]) return;
+  const int64_t row = static_cast<int64_t>(seg) * K + k;
+  const void* rec = reinterpret_cast<const void*>(to_const<uint64_t>(tab.cptrs)[row]);
+  const double norm = to_const<double>(rec)[0];
+  const int level = to_const<int32_t>(rec)[2];
+  const double w = to_const<double>(tab.w)[row];
+  const int s = static_cast<int>(threadIdx.x);
+  qtab[row * kQsgdTable + s] = __builtin_fabs(qsgd_product<DQ>(norm, level, s, w));
+}
+
+__device__ __forceinline__ void wait_vmcnt0() {
+  // s_waitcnt vmcnt(0) (expcnt / lgkmcnt: no wait): every vector memory op of this wave landed,
+  // LDS-DMA included (the compiler does not track those)
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
 }
 
 template <int OUT, typename DQ, bool FULL, bool VEC>
@@ -951,21 +945,25 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   }
 
   // Client loads of one group (slots + sign words), issued one group ahead of its fold so the
-  // HBM latency of group g+1 hides under the table build and fold of group g.
+  // HBM latency of group g+1 hides under the fold of group g. The group's |product| tables
+  // (built once per call by qsgd_table_kernel) go global -> LDS by DMA in the same step: wave w
+  // moves client k + w's 2 KiB table (two 1-KiB global_load_lds_dwordx4), the last client again
+  // for a short group, so every wave issues the same two DMAs.
   struct GroupRegs {
     u32x4 slots[kQsgdGroup];
     uint32_t signs[kQsgdGroup];
     double nrm[kQsgdGroup], wk[kQsgdGroup];  // wave-uniform (SGPRs): record header, weight
-    int lvl[kQsgdGroup];
   };
-  auto issue = [&](GroupRegs& r, int k) {
+  const int wave = __builtin_amdgcn_readfirstlane(li >> 6);
+  const int lane = li & 63;
+  const double* const tabs = a.qtab + static_cast<int64_t>(seg) * a.K * kQsgdTable;
+  auto issue = [&](GroupRegs& r, int buf, int k) {
     const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
 #pragma unroll
     for (int c = 0; c < kQsgdGroup; ++c) {
       const int kc = k + min(c, n - 1);
       const uint64_t rec = cp[kc];
       r.nrm[c] = to_const<double>(reinterpret_cast<const void*>(rec))[0];
-      r.lvl[c] = to_const<int32_t>(reinterpret_cast<const void*>(rec))[2];
       r.wk[c] = wp[kc];
       if (lane_live) {
         const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(cp[kc]));
@@ -980,8 +978,14 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
         r.signs[c] = 0xffffu;
       }
     }
+    const double* src = tabs + static_cast<int64_t>(k + min(wave, n - 1)) * kQsgdTable;
+    double* dst = lut[buf][wave];
+    __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 128 + 2 * lane),
+                                     (void __attribute__((address_space(3)))*)(dst + 128), 16, 0, 0);
   };
-  // Table build + fold of one group into LDS buffer B (compile-time, so every table read is
+  // Fold of one group from LDS buffer B (compile-time, so every table read is
   // `ds_read_b64 v, v_off offset:<buffer base>`). The table holds |p|; the sign of each
   // product is sign(x_hat) ^ sign(w) = (element negative) ^ signbit(norm) ^ signbit(w)
   // (every step of the dequantisation and the product is sign-symmetric, zeros included),
@@ -989,23 +993,11 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   auto run = [&](auto buf_tag, const GroupRegs& r, int k) {
     constexpr int B = decltype(buf_tag)::value;
     const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
-    uint32_t neg[kQsgdGroup];  // per element: 1 = the product is negative (bit layout of signs)
-#pragma unroll
-    for (int c = 0; c < kQsgdGroup; ++c) {
-      const double nrm = r.nrm[c], wk = r.wk[c];
-      // this group's product tables: lane li tabulates slot value li of every client
-#if FEDAVG_QSGD_ABLATE == 2  // timing only: no table build (wrong results)
-      lut[B][c][li] = nrm * wk;
-#else
-      lut[B][c][li] = __builtin_fabs(qsgd_product<DQ>(nrm, r.lvl[c], li, wk));
-#endif
-      const bool flip = __builtin_signbit(nrm) != __builtin_signbit(wk);  // wave-uniform
-      neg[c] = flip ? r.signs[c] : ~r.signs[c];
-    }
-    __syncthreads();
 #pragma unroll
     for (int c = 0; c < kQsgdGroup; ++c) {
       if (c < n) {
+        const bool flip = __builtin_signbit(r.nrm[c]) != __builtin_signbit(r.wk[c]);  // wave-uniform
+        const uint32_t neg = flip ? r.signs[c] : ~r.signs[c];  // per element: 1 = negative product
         const char* tab = reinterpret_cast<const char*>(lut[B][c]);
         // all 16 table reads of this client in flight before the first add (the compiler
         // otherwise keeps ~4 outstanding and waits on each batch)
@@ -1028,7 +1020,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
           // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte of
           // the little-endian 16-bit sign word, element j >= 8 bit 15 - (j - 8)
           const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
-          const uint32_t sb = neg[c] << (31 - bit);
+          const uint32_t sb = neg << (31 - bit);
           const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pav[j]));
           const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
           const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
@@ -1037,17 +1029,24 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
       }
     }
   };
-  // Two groups per iteration (LDS buffers 0 / 1): the next group's tables go into the other
-  // buffer, and the barrier before its fold orders the reuse (every lane has finished the fold
-  // two groups back). Loads run one group ahead.
+  // Two groups per iteration (LDS buffers 0 / 1). At the top of each step a wave waits for
+  // everything it issued (the group's loads and table DMAs), and the barrier publishes every
+  // wave's DMAs; only then is the next group issued into the other buffer, which the barrier
+  // also proves every wave has finished reading (its fold was two steps back).
   GroupRegs r0, r1;
-  if (kseg > 0) issue(r0, 0);
+  if (kseg > 0) issue(r0, 0, 0);
   for (int k = 0; k < kseg; k += 2 * kQsgdGroup) {
     const bool second = k + kQsgdGroup < kseg;
-    if (second) issue(r1, k + kQsgdGroup);
+    wait_vmcnt0();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (second) issue(r1, 1, k + kQsgdGroup);
     run(std::integral_constant<int, 0>{}, r0, k);
     if (second) {
-      if (k + 2 * kQsgdGroup < kseg) issue(r0, k + 2 * kQsgdGroup);
+      wait_vmcnt0();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 2 * kQsgdGroup < kseg) issue(r0, 0, k + 2 * kQsgdGroup);
       run(std::integral_constant<int, 1>{}, r1, k + kQsgdGroup);
     }
   }
@@ -1423,6 +1422,9 @@ struct fedavg_ctx {
   char* aux_host = nullptr;
   char* aux_dev = nullptr;
   size_t aux_cap = 0;
+  // QSGD |product| tables of the current call ([T][K][256] fp64, qsgd_table_kernel)
+  double* qtab = nullptr;
+  size_t qtab_cap = 0;  // doubles
   hipEvent_t aux_done = nullptr;  // the last upload out of aux_host finished
   bool aux_used = false;
 };
@@ -1774,7 +1776,16 @@ hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int
 bool is_qsgd(int32_t dt) { return dt == FEDAVG_QSGD_F32 || dt == FEDAVG_QSGD_F64; }
 
 template <int OUT>
-hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1) {
+hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1, int32_t seg_begin,
+                           int32_t seg_count) {
+  // the call's |product| tables first (same stream: the tile kernel reads them by DMA)
+  const dim3 tgrid(static_cast<unsigned>(a.K), static_cast<unsigned>(seg_count));
+  if (in_dtype == FEDAVG_QSGD_F32)
+    hipLaunchKernelGGL(qsgd_table_kernel<float>, tgrid, dim3(kQsgdTable), 0, s, a.tab, a.K, seg_begin,
+                       const_cast<double*>(a.qtab));
+  else
+    hipLaunchKernelGGL(qsgd_table_kernel<double>, tgrid, dim3(kQsgdTable), 0, s, a.tab, a.K, seg_begin,
+                       const_cast<double*>(a.qtab));
   const dim3 grid(static_cast<unsigned>(a.num_tiles)), block(kQsgdLanes);
   if (in_dtype == FEDAVG_QSGD_F32) {
     if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true>), grid, block, 0, s, nullptr, e1, 0, a);
@@ -1810,6 +1821,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   a.K = st.stride;
   a.zero_init = zero_init;
   a.walk_back = 0;
+  a.qtab = nullptr;
   int tb = 0, te = 0;
   if (split == 4) {
     // whole-layout launches only (tile ranges are defined on the SPLIT=1 table)
@@ -1881,10 +1893,23 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     a.tile_begin = tb_split1;
     a.num_tiles = te_split1 - tb_split1;
     if (a.num_tiles <= 0) return FEDAVG_OK;
+    // tables for the segments the launch's tiles touch, in a ctx buffer sized [T][K][256]
+    const size_t need = static_cast<size_t>(c->T) * static_cast<size_t>(a.K) * kQsgdTable;
+    if (c->qtab_cap < need) {
+      FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // an earlier launch may still read the old tables
+      if (c->qtab) FEDAVG_HIP_TRY(hipFree(c->qtab));
+      c->qtab = nullptr;
+      c->qtab_cap = 0;
+      FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->qtab), need * sizeof(double)));
+      c->qtab_cap = need;
+    }
+    a.qtab = c->qtab;
+    const int32_t seg0 = c->tiles1[tb_split1].seg;
+    const int32_t nseg = c->tiles1[te_split1 - 1].seg - seg0 + 1;
     switch (out_kind) {
-      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1); break;
-      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1); break;
-      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1); break;
+      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
+      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
+      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
       default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
     }
     if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
@@ -2162,6 +2187,7 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   if (c->d_tilesw_bal) (void)hipFree(c->d_tilesw_bal);
   if (c->d_tiles1_bal) (void)hipFree(c->d_tiles1_bal);
   if (c->d_segs) (void)hipFree(c->d_segs);
+  if (c->qtab) (void)hipFree(c->qtab);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->owns_acc && c->acc) (void)hipFree(c->acc);
   if (c->aux_host) (void)hipHostFree(c->aux_host);

@@ -85,6 +85,12 @@ constexpr int kU = PERS_U;             // clients loaded ahead per lane
 #ifndef PERS_RING_UNROLL  // clients of a ring stage folded per unrolled step (VGPR pressure)
 #define PERS_RING_UNROLL 1
 #endif
+#ifndef PERS_RING_WEIGHTS  // 1: the ring stages carry each wave's weight rows too (LDS broadcast reads)
+#define PERS_RING_WEIGHTS 0
+#endif
+#ifndef PERS_RING_MULADD  // 1: the mul + add fold (float weights) streams through the ring as well
+#define PERS_RING_MULADD 0
+#endif
 
 struct PChunk {
   int32_t seg;
@@ -396,6 +402,17 @@ __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, in
   // the others none) — each wave waits for its own DMAs only, the barrier for the rest
   const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
   const int nst = a.Npad / kSC;
+#if PERS_RING_WEIGHTS
+  // Each stage also carries this wave's 16 weights of each of its kSC clients (kSC x 128 B): one
+  // more DMA per wave and stage (lanes 0-31; lanes 32-63 repeat them into a copy nobody reads).
+  // The fold then reads them from LDS (broadcast reads) instead of waiting on scalar loads
+  // from L2 for every client — the weight row is in LDS a few stages before it is needed.
+  char* const wring = ring + kRS * kSC * G::kSlice;  // [kRS][waves][1 KiB]
+  const double* const wsrc = a.w + wave * kJB + 2 * (lane & 7);
+  constexpr int kWIPS = 1;  // weight DMAs per wave and stage
+#else
+  constexpr int kWIPS = 0;
+#endif
   auto issue = [&](int st) {
     char* stage = ring + (st % kRS) * (kSC * G::kSlice);
     for (int i = 0; i < per; ++i) {
@@ -403,19 +420,32 @@ __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, in
       const uint64_t p = ptrs[st * kSC + c];
       G::issue(p ? p + sb : zeros, lane, stage + c * G::kSlice);
     }
+#if PERS_RING_WEIGHTS
+    const int c = (lane >> 3) & (kSC - 1);
+    __builtin_amdgcn_global_load_lds((void PERS_AS_GLOBAL*)(wsrc + static_cast<int64_t>(st * kSC + c) * a.wstride),
+                                     (void __attribute__((address_space(3)))*)(wring + ((st % kRS) * waves + wave) * 1024),
+                                     16, 0, 0);
+#endif
   };
   for (int st = 0; st < kD && st < nst; ++st) issue(st);
   for (int st = 0; st < nst; ++st) {
     if (st + kD < nst) issue(st + kD);
     const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;  // stages issued after st
-    wait_vmcnt(ahead * per * G::kIPC);  // this wave's slices of stage st have landed
+    wait_vmcnt(ahead * (per * G::kIPC + kWIPS));  // this wave's slices of stage st have landed
     __builtin_amdgcn_s_barrier();        // ... and every other wave's
     const char* stage = ring + (st % kRS) * (kSC * G::kSlice);
+#if PERS_RING_WEIGHTS
+    const double* const wst = reinterpret_cast<const double*>(wring + ((st % kRS) * waves + wave) * 1024);
+#endif
 #pragma unroll kRingUnroll
     for (int c = 0; c < kSC; ++c) {
       double x[kVE];
       G::read(stage + c * G::kSlice, lane, x);
+#if PERS_RING_WEIGHTS
+      const double* wk = wst + c * kJB;
+#else
       const kp<double> wk = wt + static_cast<int64_t>(st * kSC + c) * a.wstride;
+#endif
 #pragma unroll
       for (int j = 0; j < kJB; ++j) {
         const double wj = wk[j];
@@ -988,9 +1018,10 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
     // the LDS ring (whole aligned fp32 / fp64 chunks) for the fused fold: measured 3.08 -> 2.85 ms
     // (64 x 64 ResNet-18); the mul + add fold is VALU-bound and ~3 % faster on the register
     // pipeline, which every other case keeps
-    a.ring = PERS_RING && fold == PF_FMA && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
+    a.ring = PERS_RING && (fold == PF_FMA || PERS_RING_MULADD) && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
     const size_t slice = static_cast<size_t>(kChunk) * (in_dtype == FEDAVG_F64 ? 8 : 4);
-    const size_t lds = sizeof(double) * 64 * kVE + (a.ring ? kRS * kSC * slice : 0);
+    const size_t lds = sizeof(double) * 64 * kVE +
+                       (a.ring ? kRS * kSC * slice + (PERS_RING_WEIGHTS ? kRS * 1024 * static_cast<size_t>(a.waves) : 0) : 0);
     const hipError_t err = launch_pers(in_dtype, a, fold, nchunks, threads, lds, s);
     if (err != hipSuccess) return pfail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
     if (p->prof) {

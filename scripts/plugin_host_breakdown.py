@@ -84,3 +84,35 @@ for _ in range(R):
         tab.rows.append(p, index, shapes, x, -1)
 out["native_rows_append_us"] = (time.perf_counter() - t0) / (R * K) * 1e6
 print(json.dumps({k: round(v, 3) for k, v in out.items()}))
+
+# aggregate_worker_data's pieces on the same 64-client table (the plugin's common path, by hand)
+from distributed_learning_simulation_lib_amd.fedavg import FedAvgContext, OutputTable  # noqa: E402
+
+ctx = FedAvgContext(layout, dev)
+offs, total = layout.padded_offsets(8)
+tab = _staging.NativeClientTable(layout.num_segments, 0)
+for p, x in zip(params, w):
+    tab.rows.append(p, index, shapes, x, -1)
+ext = _staging.module()
+t_alloc = t_enq = t_sync = t_flags = t_views = 0.0
+for _ in range(R + 3):
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    flat = torch.empty(total, dtype=torch.float64, device=dev)
+    ot = OutputTable.from_flat(flat, offs, layout)
+    b = time.perf_counter()
+    ctx.aggregate(tab, torch.float32, ot, torch.float64)
+    c = time.perf_counter()
+    torch.cuda.synchronize()
+    d = time.perf_counter()
+    ctx.raise_on_nan([])
+    e = time.perf_counter()
+    ext.views(flat, offs, shapes)
+    f = time.perf_counter()
+    ctx.reset()
+    if _ >= 3:
+        t_alloc, t_enq, t_sync, t_flags, t_views = (t_alloc + b - a, t_enq + c - b, t_sync + d - c, t_flags + e - d,
+                                                     t_views + f - e)
+out2 = {"alloc_outputs_us": t_alloc / R * 1e6, "aggregate_enqueue_us": t_enq / R * 1e6,
+        "kernel_wait_us": t_sync / R * 1e6, "flags_us": t_flags / R * 1e6, "views_us": t_views / R * 1e6}
+print(json.dumps({k: round(v, 2) for k, v in out2.items()}))

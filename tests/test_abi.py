@@ -1,6 +1,8 @@
 """The C ABI surface: header <-> binding <-> exported symbols (CPU only, no compute calls)."""
 
 import re
+
+import pytest
 import subprocess
 from pathlib import Path
 
@@ -55,3 +57,20 @@ def test_layout_acc_numel_aligns_segments():
     want = sum((n + _native.ACC_ALIGN - 1) // _native.ACC_ALIGN * _native.ACC_ALIGN for n in numels)
     assert lib.fedavg_layout_acc_numel(arr, len(numels)) == want
     assert lib.fedavg_layout_acc_numel(arr, 0) == -1
+
+
+def test_kernel_constants_are_readable_without_a_gpu():
+    """fedavg_kernel_constant: the geometry the GPU property tests place their sizes around."""
+    from distributed_learning_simulation_lib_amd._native import NativeError, kernel_constant
+
+    assert kernel_constant("tile") == 4096 and kernel_constant("tile_wide") in (0, 4096, 8192)
+    for d in ("f32", "f16", "bf16", "f64"):
+        ae, lanes = kernel_constant(f"ae_{d}"), kernel_constant(f"lanes_{d}")
+        assert ae > 0 and lanes % 64 == 0 and kernel_constant(f"group_{d}") >= 2
+        assert kernel_constant(f"ae4096_{d}") * kernel_constant(f"lanes4096_{d}") == 4096
+        assert kernel_constant(f"pipe_{d}") >= 0
+    assert kernel_constant("pers_group") % kernel_constant("pers_jb") == 0
+    assert kernel_constant("qsgd_tile") == kernel_constant("qsgd_ae") * 256
+    for bad in ("nope", "ae_f8", "pers_nope", ""):
+        with pytest.raises(NativeError):
+            kernel_constant(bad)

@@ -1,7 +1,7 @@
-"""The epilogue / QSGD-table division identity (csrc/exact_div.h) checked on the host:
-scripts/check_exact_div.c compiled with gcc (hardware fma) over 3 x 2e6 quotients — random
-binary64, binary64 near the quotient grid's midpoints, binary32 over the QSGD levels — must equal
-IEEE division bit for bit. (The GPU suite checks the kernels themselves against the oracle.)"""
+"""The epilogue division identity (csrc/exact_div.h) checked on the host: scripts/check_exact_div.c
+compiled with gcc (hardware fma) over 2 x 2e6 quotients — random binary64 over the fast path's
+whole range, binary64 near the quotient grid's midpoints — must equal IEEE division bit for bit.
+(The GPU suite checks the kernels themselves against the oracle.)"""
 
 from __future__ import annotations
 

@@ -17,6 +17,8 @@ from .build import LIB_PATH
 # enum fedavg_dtype
 F32, F16, BF16, F64 = 0, 1, 2, 3
 QSGD_F32, QSGD_F64 = 4, 5  # quantised records (quantized.py)
+NNADQ_F32, NNADQ_F64 = 6, 7
+RECORD_CODES = (QSGD_F32, QSGD_F64, NNADQ_F32, NNADQ_F64)
 # enum fedavg_status
 OK = 0
 ERR_NAN_INPUT = 1
@@ -48,6 +50,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_last_error": (ctypes.c_char_p, []),
     "fedavg_qsgd_record_bytes": (c_int64, [c_int64]),
     "fedavg_qsgd_sign_offset": (c_int64, [c_int64]),
+    "fedavg_nnadq_record_bytes": (c_int64, [c_int64]),
     "fedavg_ctx_create": (
         c_int32,
         [POINTER(c_void_p), c_int32, POINTER(c_int64), c_int32, c_void_p],

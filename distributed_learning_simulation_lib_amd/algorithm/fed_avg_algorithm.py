@@ -135,7 +135,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__has_data = False
         self.__ingest: HostIngest | None = None
         self.__result_flat: torch.Tensor | None = None
-        self.__record_layouts: dict[tuple[int, ...], ModelLayout] = {}
+        self.__record_layouts: dict[tuple, ModelLayout] = {}
         # fed_avg_algorithm.py:59-62, kept with the hook's own objects (scalar weights)
         self.__host_totals: dict[str, Any] = {}
         # while every staged update of the round carried every name of the layout, all per-name
@@ -631,8 +631,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             ]
         return [None if t is None else to_device_operand(t, self.device) for t in tensors]
 
-    # Quantised updates (StochasticQuantServerEndpoint, quantized_endpoint.py:69-77,102-111) are
-    # handed over as QSGD records; the kernel dequantises them inside the fold.
+    # Quantised updates (StochasticQuantServerEndpoint / NNADQServerEndpoint, quantized_endpoint.py:
+    # 69-77,102-142) are handed over as QSGD / NNADQ records; the kernel dequantises them inside
+    # the fold.
     accepts_quantized_messages = True
 
     def _host_records_to_device(self, tensors: list, recs: list) -> tuple[list[int], list[int], list]:
@@ -641,9 +642,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if self.__ingest is None:
             self.__ingest = HostIngest(self.device)
         numels = tuple(1 if q is None else q.numel for q in tensors)
-        rl = self.__record_layouts.get(numels)
+        codec = next(q.codec for q in tensors if q is not None)
+        rl = self.__record_layouts.get((numels, codec))
         if rl is None:
-            rl = self.__record_layouts[numels] = record_layout(list(numels))
+            rl = self.__record_layouts[(numels, codec)] = record_layout(list(numels), codec)
         nums = [-1 if r is None else r.numel() for r in recs]
         bucket, dptrs = self.__ingest.to_device_pointers(rl, [0 if r is None else r.data_ptr() for r in recs],
                                                          nums, torch.uint8)
@@ -658,9 +660,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             if self.__ingest is None:
                 self.__ingest = HostIngest(self.device)
             numels = tuple(q.numel if q is not None else 1 for q in tensors)
-            rl = self.__record_layouts.get(numels)
+            codec = host[0].codec
+            rl = self.__record_layouts.get((numels, codec))
             if rl is None:
-                rl = self.__record_layouts[numels] = record_layout(list(numels))
+                rl = self.__record_layouts[(numels, codec)] = record_layout(list(numels), codec)
             staged = self.__ingest.to_device(
                 rl,
                 [q.record if q is not None and q.device.type == "cpu" else None for q in tensors],
@@ -813,19 +816,20 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 else:
                     ctx.set_accumulated([float(self.__host_totals[layout.names[i]]) for i in self.__keep])
                     ctx.finalize_range(outs, out_dtype)
-            ctx.raise_on_nan(pending)
+            result: ModelParameter = {}
+            if not custom_divide:
+                # the segments as shaped views of the flat result (one native call when the staging
+                # extension is built), made while the kernel runs
+                ext = _staging.module()
+                views = ext.views(flat, offs, shapes) if ext is not None else \
+                    [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+                for j, i in enumerate(self.__keep):
+                    result[layout.names[i]] = views[j]
+            ctx.raise_on_nan(pending)  # the round ends on the host: :93 / :97 asserted
         except NaNAggregationError:
             ctx.reset()
             raise
-        result: ModelParameter = {}
-        ext = _staging.module()
         if not custom_divide:
-            # the segments as shaped views of the flat result (one native call when the staging
-            # extension is built)
-            views = ext.views(flat, offs, shapes) if ext is not None else \
-                [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
-            for j, i in enumerate(self.__keep):
-                result[layout.names[i]] = views[j]
             ctx.reset()
             return result
         # a subclass's _apply_total_weight runs where the reference runs it — on host fp64

@@ -139,9 +139,6 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 #ifndef FEDAVG_BALANCE_DEFAULT  // balanced whole-layout tile orders (bit 0 fp32, bit 1 fp64); env FEDAVG_BALANCE
 #define FEDAVG_BALANCE_DEFAULT 3
 #endif
-#ifndef FEDAVG_PARTV  // 1 = tiles of whole lane-vectors take the grouped fast path (A/B knob; pair 0 with
-#define FEDAVG_PARTV 1  // FEDAVG_BALANCE_DEFAULT=0, whose pieces are such tiles)
-#endif
 #ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
 #define FEDAVG_ACC_NT_LOAD 0
 #endif
@@ -799,7 +796,11 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   }
 }
 
-template <typename T, int OUT, int SPLIT, bool VEC, int FOLD, int TILEN = kTile1>
+// PV: the launch's tile table holds tiles of whole lane-vectors shorter than a tile (the pieces of
+// a balanced order, build_balanced_tiles) and they take the grouped fast path. A separate
+// instantiation: compiled into every launch, that path cost the plain whole-layout launch 3-4 %
+// (VGPRs 131 -> 144, twice the code; profiles/r03_ab_matrix.txt).
+template <typename T, int OUT, int SPLIT, bool VEC, int FOLD, int TILEN = kTile1, bool PV = false>
 __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
   constexpr int TILE = Geo<T, SPLIT, TILEN>::TILE;
@@ -815,10 +816,9 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
       tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN>(a, td, lds);
     } else {
       bool partv = false;
-      if constexpr (SPLIT == 1 && VEC && LV < TILE && FEDAVG_PARTV) partv = (td.count % LV) == 0;
+      if constexpr (PV && SPLIT == 1 && VEC && LV < TILE) partv = (td.count % LV) == 0;
       if (partv) {
-        if constexpr (SPLIT == 1 && VEC && LV < TILE && FEDAVG_PARTV)
-          tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN, true>(a, td, lds);
+        if constexpr (PV && SPLIT == 1 && VEC && LV < TILE) tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN, true>(a, td, lds);
       } else {
         tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN>(a, td, lds);
       }
@@ -907,6 +907,95 @@ __device__ __forceinline__ void wait_vmcnt0() {
   __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
 }
 
+// Continuing accumulator of a record tile (lane slice [e0, e0 + AE) of the tile), or the -0.0
+// identity. Returns whether the accumulator held data.
+template <bool FULL, int AE>
+__device__ __forceinline__ bool record_tile_acc_in(const KArgs& a, int seg, int64_t acc_base, int e0, int count,
+                                                   double (&acc)[AE]) {
+#pragma unroll
+  for (int i = 0; i < AE; ++i) acc[i] = -0.0;  // additive identity (see tile_body)
+  if (a.zero_init || !to_const<int32_t>(a.tab.acc_in)[seg]) return a.zero_init != 0;
+  const gptr<const double> ap = to_global<double>(a.acc + acc_base) + e0;
+#pragma unroll
+  for (int j = 0; j < AE; j += 2) {
+    if (FULL || e0 + j + 2 <= count) {
+      const f64x2 d = *(gptr<const f64x2>)(ap + j);
+      acc[j] = d.x;
+      acc[j + 1] = d.y;
+    } else {
+      if (e0 + j < count) acc[j] = ap[j];
+      if (e0 + j + 1 < count) acc[j + 1] = ap[j + 1];
+    }
+  }
+  return true;
+}
+
+// Epilogue of a record tile (QSGD / NNADQ kernels): store the lane's fp64 accumulator slice, or
+// divide it by the segment's total weight (exact_div_block) into the fp32 / fp64 output; NaN
+// flags as in tile_body.
+template <int OUT, bool FULL, bool VEC, int AE>
+__device__ __forceinline__ void record_tile_finish(const KArgs& a, const TileDesc& td, int64_t acc_base, int e0,
+                                                   const double (&acc)[AE]) {
+  const int seg = td.seg;
+  const int count = td.count;
+  bool bad_acc = false;
+#pragma unroll
+  for (int j = 0; j < AE; ++j) bad_acc |= (FULL || e0 + j < count) && (acc[j] != acc[j]);
+
+  if constexpr (OUT == OUT_ACC) {
+    const gptr<double> ap = to_global_mut<double>(a.acc + acc_base) + e0;
+#pragma unroll
+    for (int j = 0; j < AE; j += 2) {
+      if (FULL || e0 + j + 2 <= count) {
+        *(gptr<f64x2>)(ap + j) = f64x2{acc[j], acc[j + 1]};
+      } else {
+        if (e0 + j < count) ap[j] = acc[j];
+        if (e0 + j + 1 < count) ap[j + 1] = acc[j + 1];
+      }
+    }
+    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) raise_flag(a.flag, 0);
+  } else {
+    const double W = to_const<double>(a.tab.wtot)[seg];
+    double res[AE];
+    bool bad_res = false;
+    exact_div_block<AE>(acc, res, W);
+#pragma unroll
+    for (int j = 0; j < AE; ++j) bad_res |= (FULL || e0 + j < count) && (res[j] != res[j]);
+    void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
+    if constexpr (OUT == OUT_F32) {
+      const gptr<float> op = to_global_mut<float>(out_raw) + td.start + e0;
+#pragma unroll
+      for (int j = 0; j < AE; j += 4) {
+        if (VEC && (FULL || e0 + j + 4 <= count)) {
+          *(gptr<f32x4>)(op + j) = f32x4{static_cast<float>(res[j]), static_cast<float>(res[j + 1]),
+                                          static_cast<float>(res[j + 2]), static_cast<float>(res[j + 3])};
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (e0 + j + q < count) op[j + q] = static_cast<float>(res[j + q]);
+        }
+      }
+    } else {
+      const gptr<double> op = to_global_mut<double>(out_raw) + td.start + e0;
+#pragma unroll
+      for (int j = 0; j < AE; j += 2) {
+        if (VEC && (FULL || e0 + j + 2 <= count)) {
+          *(gptr<f64x2>)(op + j) = f64x2{res[j], res[j + 1]};
+        } else {
+          if (e0 + j < count) op[j] = res[j];
+          if (e0 + j + 1 < count) op[j + 1] = res[j + 1];
+        }
+      }
+    }
+    const uint64_t ba = __ballot(bad_acc);
+    const uint64_t br = __ballot(bad_res);
+    if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+      if (ba) raise_flag(a.flag, 0);
+      if (br) raise_flag(a.flag, 1);
+    }
+  }
+}
+
 template <int OUT, typename DQ, bool FULL, bool VEC>
 __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable]) {
   constexpr int AE = kQsgdAE;
@@ -925,24 +1014,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   const int64_t sign_off = 16 + ((numel + 15) & ~int64_t(15)) + (td.start + e0) / 8;
 
   double acc[AE];
-#pragma unroll
-  for (int i = 0; i < AE; ++i) acc[i] = -0.0;  // additive identity (see tile_body)
-  bool have = a.zero_init != 0;
-  if (!a.zero_init && to_const<int32_t>(a.tab.acc_in)[seg]) {
-    const gptr<const double> ap = to_global<double>(a.acc + acc_base) + e0;
-#pragma unroll
-    for (int j = 0; j < AE; j += 2) {
-      if (FULL || e0 + j + 2 <= count) {
-        const f64x2 d = *(gptr<const f64x2>)(ap + j);
-        acc[j] = d.x;
-        acc[j + 1] = d.y;
-      } else {
-        if (e0 + j < count) acc[j] = ap[j];
-        if (e0 + j + 1 < count) acc[j + 1] = ap[j + 1];
-      }
-    }
-    have = true;
-  }
+  bool have = record_tile_acc_in<FULL, AE>(a, seg, acc_base, e0, count, acc);
 
   // Client loads of one group (slots + sign words), issued one group ahead of its fold so the
   // HBM latency of group g+1 hides under the fold of group g. The group's |product| tables
@@ -1052,63 +1124,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   }
   have = have || (kseg > 0);
   if (!have) return;
-
-  bool bad_acc = false;
-#pragma unroll
-  for (int j = 0; j < AE; ++j) bad_acc |= (FULL || e0 + j < count) && (acc[j] != acc[j]);
-
-  if constexpr (OUT == OUT_ACC) {
-    const gptr<double> ap = to_global_mut<double>(a.acc + acc_base) + e0;
-#pragma unroll
-    for (int j = 0; j < AE; j += 2) {
-      if (FULL || e0 + j + 2 <= count) {
-        *(gptr<f64x2>)(ap + j) = f64x2{acc[j], acc[j + 1]};
-      } else {
-        if (e0 + j < count) ap[j] = acc[j];
-        if (e0 + j + 1 < count) ap[j + 1] = acc[j + 1];
-      }
-    }
-    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) raise_flag(a.flag, 0);
-  } else {
-    const double W = to_const<double>(a.tab.wtot)[seg];
-    double res[AE];
-    bool bad_res = false;
-    exact_div_block<AE>(acc, res, W);
-#pragma unroll
-    for (int j = 0; j < AE; ++j) bad_res |= (FULL || e0 + j < count) && (res[j] != res[j]);
-    void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
-    if constexpr (OUT == OUT_F32) {
-      const gptr<float> op = to_global_mut<float>(out_raw) + td.start + e0;
-#pragma unroll
-      for (int j = 0; j < AE; j += 4) {
-        if (VEC && (FULL || e0 + j + 4 <= count)) {
-          *(gptr<f32x4>)(op + j) = f32x4{static_cast<float>(res[j]), static_cast<float>(res[j + 1]),
-                                          static_cast<float>(res[j + 2]), static_cast<float>(res[j + 3])};
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (e0 + j + q < count) op[j + q] = static_cast<float>(res[j + q]);
-        }
-      }
-    } else {
-      const gptr<double> op = to_global_mut<double>(out_raw) + td.start + e0;
-#pragma unroll
-      for (int j = 0; j < AE; j += 2) {
-        if (VEC && (FULL || e0 + j + 2 <= count)) {
-          *(gptr<f64x2>)(op + j) = f64x2{res[j], res[j + 1]};
-        } else {
-          if (e0 + j < count) op[j] = res[j];
-          if (e0 + j + 1 < count) op[j + 1] = res[j + 1];
-        }
-      }
-    }
-    const uint64_t ba = __ballot(bad_acc);
-    const uint64_t br = __ballot(bad_res);
-    if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
-      if (ba) raise_flag(a.flag, 0);
-      if (br) raise_flag(a.flag, 1);
-    }
-  }
+  record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
 }
 
 template <int OUT, typename DQ, bool VEC>
@@ -1140,6 +1156,149 @@ __global__ __launch_bounds__(kThreads) void qsgd_nan_scan_kernel(const TileDesc*
     b |= (x != x);
   }
   (void)segs;
+  if (__ballot(b) != 0ull && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned*>(bad + k), 1u);
+}
+
+// ---------------------------------------------------------------------------------------
+// NNADQ records (NNADQServerEndpoint, simulation_lib/topology/quantized_endpoint.py:114-142:
+// the deterministic codec of the unvendored cyy_torch_algorithm.quantization.deterministic,
+// dequantised by QuantServerEndpoint.get, :69-77, before the fold). The record is the client
+// "tensor" here too:
+//
+//   record (16-B aligned, fedavg_nnadq_record_bytes(n) = 32 + align16(n) bytes):
+//     [0, 8)   lo (fp64; holds the fp32 value exactly for FEDAVG_NNADQ_F32)
+//     [8, 16)  step (fp64, likewise)
+//     [16, 20) levels (int32, 1..255; informational — codes are never above it)
+//     [32, 32 + n)  codes, one uint8 per element
+//
+//   x_hat = code * step + lo in the codec's dtype, two roundings (-ffp-contract=off)
+//
+// No table: one multiply and one add in the codec's dtype is cheaper than a table read, so each
+// element is dequantised in registers and folded like a dense input, FOLD kinds included (the
+// fused fold when the host proves every x * w exact — fp32 codec values and integer weights).
+// HBM carries 1 B per element per client. Geometry: 256-lane workgroups on the 4096-element
+// tiles, lane li owns elements [16 li, 16 li + 16) (one 16-B code load per client: a wave reads
+// 1 KiB contiguously); clients in groups of kNnadqGroup, group g + 1's loads issued before group
+// g's fold (a register double buffer; no LDS, no barriers).
+constexpr int kNnadqHeader = 32;
+constexpr int kNnadqLanes = 256;
+constexpr int kNnadqAE = 16;
+#ifndef FEDAVG_NNADQ_GROUP
+#define FEDAVG_NNADQ_GROUP 8
+#endif
+constexpr int kNnadqGroup = FEDAVG_NNADQ_GROUP;
+static_assert(kNnadqLanes * kNnadqAE == kTile1, "NNADQ launches walk the 4096-element tile table");
+
+template <typename DQ>
+__device__ __forceinline__ double nnadq_value(uint32_t code, DQ step, DQ lo) {
+  const DQ c = static_cast<DQ>(code);
+  const DQ p = c * step;  // rounded in the codec's dtype
+  const DQ v = p + lo;    // rounded again (no contraction)
+  return static_cast<double>(v);  // .to(float64), fed_avg_algorithm.py:54
+}
+
+template <int OUT, typename DQ, int FOLD, bool FULL, bool VEC>
+__device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& td) {
+  constexpr int AE = kNnadqAE;
+  constexpr int G = kNnadqGroup;
+  const int seg = td.seg;
+  const int count = td.count;
+  const int li = static_cast<int>(threadIdx.x);
+  const int e0 = li * AE;
+  const bool lane_live = FULL || e0 < count;  // a 16-B load at e0 < numel stays in the record
+
+  const int kseg = to_const<int32_t>(a.tab.kseg)[seg];
+  const kptr<uint64_t> cp = to_const<uint64_t>(a.tab.cptrs) + static_cast<int64_t>(seg) * a.K;
+  const kptr<double> wp = to_const<double>(a.tab.w) + static_cast<int64_t>(seg) * a.K;
+  const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;
+  const int64_t code_off = kNnadqHeader + td.start + e0;
+
+  double acc[AE];
+  bool have = record_tile_acc_in<FULL, AE>(a, seg, acc_base, e0, count, acc);
+
+  struct GroupRegs {
+    u32x4 codes[G];
+    DQ lo[G], step[G];  // wave-uniform (SGPRs): record header
+    double wk[G];
+  };
+  auto issue = [&](GroupRegs& r, int k) {
+    const int n = min(G, kseg - k);  // wave-uniform
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c < n) {
+        const uint64_t rec = cp[k + c];
+        const kptr<double> hdr = to_const<double>(reinterpret_cast<const void*>(rec));
+        r.lo[c] = static_cast<DQ>(hdr[0]);
+        r.step[c] = static_cast<DQ>(hdr[1]);
+        r.wk[c] = wp[k + c];
+        if (lane_live) {
+          const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(rec));
+#if FEDAVG_NT
+          r.codes[c] = __builtin_nontemporal_load((gptr<const u32x4>)(rp + code_off));
+#else
+          r.codes[c] = *(gptr<const u32x4>)(rp + code_off);
+#endif
+        } else {
+          r.codes[c] = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+    }
+  };
+  auto run = [&](const GroupRegs& r, int k) {
+    const int n = min(G, kseg - k);  // wave-uniform
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c < n) {
+#pragma unroll
+        for (int j = 0; j < AE; ++j) {
+          const uint32_t code = (r.codes[c][j >> 2] >> (8 * (j & 3))) & 0xffu;
+          acc[j] = fold<FOLD>(acc[j], nnadq_value<DQ>(code, r.step[c], r.lo[c]), r.wk[c], 0.0);
+        }
+      }
+    }
+  };
+  GroupRegs r0, r1;
+  if (kseg > 0) issue(r0, 0);
+  for (int k = 0; k < kseg; k += 2 * G) {
+    const bool second = k + G < kseg;
+    if (second) issue(r1, k + G);
+    run(r0, k);
+    if (second) {
+      if (k + 2 * G < kseg) issue(r0, k + 2 * G);
+      run(r1, k + G);
+    }
+  }
+  have = have || (kseg > 0);
+  if (!have) return;
+  record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
+}
+
+template <int OUT, typename DQ, int FOLD, bool VEC>
+__global__ __launch_bounds__(kNnadqLanes) void nnadq_tile_kernel(KArgs a) {
+  const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
+  if (td.count == kTile1) {
+    nnadq_tile_body<OUT, DQ, FOLD, true, VEC>(a, td);
+  } else {
+    nnadq_tile_body<OUT, DQ, FOLD, false, VEC>(a, td);
+  }
+}
+
+// Diagnostic for NNADQ clients: which record dequantises to a NaN somewhere.
+template <typename DQ>
+__global__ __launch_bounds__(kThreads) void nnadq_nan_scan_kernel(const TileDesc* tiles, const void* const* cptrs_tk,
+                                                                 int32_t K, int32_t* bad) {
+  const TileDesc td = load_tile(tiles, blockIdx.x);
+  const int k = blockIdx.y;
+  const uint64_t raw = to_const<uint64_t>(cptrs_tk)[static_cast<int64_t>(td.seg) * K + k];
+  if (raw == 0) return;
+  const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(raw));
+  const DQ lo = static_cast<DQ>(*(gptr<const double>)rp);
+  const DQ step = static_cast<DQ>(*(gptr<const double>)(rp + 8));
+  bool b = false;
+  for (int i = threadIdx.x; i < td.count; i += kThreads) {
+    const double x = nnadq_value<DQ>(rp[kNnadqHeader + td.start + i], step, lo);
+    b |= (x != x);
+  }
   if (__ballot(b) != 0ull && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned*>(bad + k), 1u);
 }
 
@@ -1439,8 +1598,10 @@ int32_t elem_size(int32_t dt) {
     case FEDAVG_F16: return 2;
     case FEDAVG_BF16: return 2;
     case FEDAVG_F64: return 8;
-    case FEDAVG_QSGD_F32: return 1;  // quantised records (slots are bytes)
+    case FEDAVG_QSGD_F32: return 1;  // quantised records (slots / codes are bytes)
     case FEDAVG_QSGD_F64: return 1;
+    case FEDAVG_NNADQ_F32: return 1;
+    case FEDAVG_NNADQ_F64: return 1;
     default: return 0;
   }
 }
@@ -1568,6 +1729,7 @@ int32_t significand_bits(int32_t dt) {
     case FEDAVG_F32: return 24;
     case FEDAVG_F16: return 11;
     case FEDAVG_BF16: return 8;
+    case FEDAVG_NNADQ_F32: return 24;  // dequantised values are fp32
     default: return 53;
   }
 }
@@ -1722,58 +1884,85 @@ int32_t aux_upload(fedavg_ctx* c, hipStream_t s, const std::vector<char>& blob, 
 // own dispatch (its completion signal) instead of a separate marker packet — a marker between
 // two kernels costs ~6-16 µs of queue latency (DESIGN.md §5 traces); the sharded round's
 // per-chunk events use this.
-template <typename T, int OUT, int SPLIT, bool VEC, int TILEN = kTile1>
-hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+template <typename T, int OUT, int SPLIT, bool VEC, int TILEN = kTile1, bool PV = false>
+hipError_t launch_fold_pv(const KArgs& a, int fold, int nblocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int threads = Geo<T, SPLIT, TILEN>::THREADS;
   if (fold == FOLD_FMA) {
-    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA, TILEN>), dim3(nblocks), dim3(threads), 0,
-                          s, e0, e1, 0, a);
+    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_FMA, TILEN, PV>), dim3(nblocks), dim3(threads),
+                          0, s, e0, e1, 0, a);
   } else if (fold == FOLD_DELTA) {
     if constexpr (SPLIT == 1) {
-      hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA, TILEN>), dim3(nblocks),
+      hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_DELTA, TILEN, PV>), dim3(nblocks),
                             dim3(threads), 0, s, e0, e1, 0, a);
     } else {
       return hipErrorInvalidValue;  // delta calls run the exact-order kernel only
     }
   } else {
-    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD, TILEN>), dim3(nblocks), dim3(threads),
-                          0, s, e0, e1, 0, a);
+    hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, SPLIT, VEC, FOLD_MULADD, TILEN, PV>), dim3(nblocks),
+                          dim3(threads), 0, s, e0, e1, 0, a);
   }
   return hipGetLastError();
+}
+
+// partv: the tile table is a balanced order (pieces of whole lane-vectors: the PV instantiation)
+template <typename T, int OUT, int SPLIT, bool VEC, int TILEN = kTile1>
+hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                       bool partv = false) {
+  if constexpr (SPLIT == 1 && VEC) {
+    if (partv) return launch_fold_pv<T, OUT, SPLIT, VEC, TILEN, true>(a, fold, nblocks, s, e0, e1);
+  }
+  return launch_fold_pv<T, OUT, SPLIT, VEC, TILEN, false>(a, fold, nblocks, s, e0, e1);
 }
 
 // wide = a whole-layout exact-order launch over the kTileWide table (2- / 4-byte inputs only)
 template <typename T, int OUT>
 hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s, hipEvent_t e0,
-                        hipEvent_t e1, bool wide) {
+                        hipEvent_t e1, bool wide, bool partv) {
   if (split == 4) {
     return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s, e0, e1)
                : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s, e0, e1);
   }
   if constexpr ((sizeof(T) < 8 || FEDAVG_F64_WIDE) && kTileWide > 0) {
     if (wide) {
-      return vec ? launch_fold<T, OUT, 1, true, kTileWide>(a, fold, nblocks, s, e0, e1)
+      return vec ? launch_fold<T, OUT, 1, true, kTileWide>(a, fold, nblocks, s, e0, e1, partv)
                  : launch_fold<T, OUT, 1, false, kTileWide>(a, fold, nblocks, s, e0, e1);
     }
   }
   if (wide) return hipErrorInvalidValue;
-  return vec ? launch_fold<T, OUT, 1, true>(a, fold, nblocks, s, e0, e1)
+  return vec ? launch_fold<T, OUT, 1, true>(a, fold, nblocks, s, e0, e1, partv)
              : launch_fold<T, OUT, 1, false>(a, fold, nblocks, s, e0, e1);
 }
 
 template <int OUT>
 hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int fold, int nblocks, hipStream_t s,
-                      hipEvent_t e0, hipEvent_t e1, bool wide) {
+                      hipEvent_t e0, hipEvent_t e1, bool wide, bool partv = false) {
   switch (in_dtype) {
-    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
-    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
-    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
-    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide);
+    case FEDAVG_F32: return launch_typed<float, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide, partv);
+    case FEDAVG_F16: return launch_typed<__half, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide, partv);
+    case FEDAVG_BF16: return launch_typed<bf16_t, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide, partv);
+    case FEDAVG_F64: return launch_typed<double, OUT>(a, split, vec, fold, nblocks, s, e0, e1, wide, partv);
     default: return hipErrorInvalidValue;
   }
 }
 
 bool is_qsgd(int32_t dt) { return dt == FEDAVG_QSGD_F32 || dt == FEDAVG_QSGD_F64; }
+bool is_nnadq(int32_t dt) { return dt == FEDAVG_NNADQ_F32 || dt == FEDAVG_NNADQ_F64; }
+bool is_record(int32_t dt) { return is_qsgd(dt) || is_nnadq(dt); }
+
+template <int OUT, typename DQ, int FOLD>
+hipError_t launch_nnadq_fold(const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1) {
+  const dim3 grid(static_cast<unsigned>(a.num_tiles)), block(kNnadqLanes);
+  if (vec) hipExtLaunchKernelGGL((nnadq_tile_kernel<OUT, DQ, FOLD, true>), grid, block, 0, s, nullptr, e1, 0, a);
+  else hipExtLaunchKernelGGL((nnadq_tile_kernel<OUT, DQ, FOLD, false>), grid, block, 0, s, nullptr, e1, 0, a);
+  return hipGetLastError();
+}
+
+template <int OUT>
+hipError_t launch_nnadq_out(int32_t in_dtype, const KArgs& a, bool vec, bool fma, hipStream_t s, hipEvent_t e1) {
+  if (in_dtype == FEDAVG_NNADQ_F32)
+    return fma ? launch_nnadq_fold<OUT, float, FOLD_FMA>(a, vec, s, e1) : launch_nnadq_fold<OUT, float, FOLD_MULADD>(a, vec, s, e1);
+  return fma ? launch_nnadq_fold<OUT, double, FOLD_FMA>(a, vec, s, e1) : launch_nnadq_fold<OUT, double, FOLD_MULADD>(a, vec, s, e1);
+}
 
 template <int OUT>
 hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1, int32_t seg_begin,
@@ -1859,7 +2048,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   // whole-layout waves alternate their walk (a balanced order reverses only its leading whole
   // waves: its short pieces stay at the end, where they balance the tail; ranged launches keep
   // their order)
-  if (c->walk_alternate && split == 1 && c->persistent_blocks == 0 && !is_qsgd(in_dtype) &&
+  if (c->walk_alternate && split == 1 && c->persistent_blocks == 0 && !is_record(in_dtype) &&
       tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
     if (c->walk_reverse)
       a.walk_back = (a.tiles == c->d_tilesw_bal)   ? c->tilesw_bal_head
@@ -1884,7 +2073,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     e1 = nullptr;
   }
   hipError_t err = hipSuccess;
-  if (is_qsgd(in_dtype)) {
+  if (is_record(in_dtype)) {
     // quantised records: one tile per workgroup, exact client order (no split, no persistent
     // grid); the record layout needs 16-B aligned records; outputs may be unaligned
     if (st.delta) return fail(FEDAVG_ERR_INVALID, "quantised records cannot be delta updates");
@@ -1893,6 +2082,23 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     a.tile_begin = tb_split1;
     a.num_tiles = te_split1 - tb_split1;
     if (a.num_tiles <= 0) return FEDAVG_OK;
+  }
+  if (is_nnadq(in_dtype)) {
+    const bool fma = c->allow_fma && fma_exact_call(st, in_dtype);
+    switch (out_kind) {
+      case OUT_ACC: err = launch_nnadq_out<OUT_ACC>(in_dtype, a, st.aligned, fma, s, e1); break;
+      case OUT_F32: err = launch_nnadq_out<OUT_F32>(in_dtype, a, st.aligned, fma, s, e1); break;
+      case OUT_F64: err = launch_nnadq_out<OUT_F64>(in_dtype, a, st.aligned, fma, s, e1); break;
+      default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
+    }
+    if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
+    if (m1) {
+      FEDAVG_HIP_TRY(hipEventRecord(m1, s));
+      if (done_ev) *done_ev = m1;
+    }
+    return FEDAVG_OK;
+  }
+  if (is_qsgd(in_dtype)) {
     // tables for the segments the launch's tiles touch, in a ctx buffer sized [T][K][256]
     const size_t need = static_cast<size_t>(c->T) * static_cast<size_t>(a.K) * kQsgdTable;
     if (c->qtab_cap < need) {
@@ -1921,10 +2127,11 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   }
   const int fold = st.delta ? FOLD_DELTA
                             : (c->allow_fma && fma_exact_call(st, in_dtype)) ? FOLD_FMA : FOLD_MULADD;
+  const bool partv = a.tiles == c->d_tilesw_bal || a.tiles == c->d_tiles1_bal;  // a balanced order
   switch (out_kind) {
-    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide); break;
-    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide); break;
-    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide); break;
+    case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide, partv); break;
+    case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide, partv); break;
+    case OUT_F64: err = launch_out<OUT_F64>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide, partv); break;
     default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
   }
   if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
@@ -1997,6 +2204,10 @@ int32_t fedavg_kernel_constant(const char* name, int64_t* out) {
   else if (n == "qsgd_tile") v = kTile1;
   else if (n == "qsgd_ae") v = kQsgdAE;
   else if (n == "qsgd_group") v = kQsgdGroup;
+  else if (n == "nnadq_tile") v = kTile1;
+  else if (n == "nnadq_ae") v = kNnadqAE;
+  else if (n == "nnadq_group") v = kNnadqGroup;
+  else if (n == "nnadq_header") v = kNnadqHeader;
   else if (n.rfind("pers_", 0) == 0) {
     if (fedavg_internal_pers_constant(name, &v) != FEDAVG_OK) v = -1;
   } else {
@@ -2039,6 +2250,11 @@ int64_t fedavg_qsgd_record_bytes(int64_t numel) {
   return fedavg_qsgd_sign_offset(numel) + static_cast<int64_t>(align_up(static_cast<size_t>((numel + 7) / 8), 16));
 }
 
+int64_t fedavg_nnadq_record_bytes(int64_t numel) {
+  if (numel < 0) return -1;
+  return kNnadqHeader + static_cast<int64_t>(align_up(static_cast<size_t>(numel), 16));
+}
+
 const char* fedavg_last_error(void) { return g_last_error.c_str(); }
 
 int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_numel,
@@ -2076,21 +2292,33 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
     // the kTile1 table), sized by the resident workgroups of the kernel that runs them
     const char* env = std::getenv("FEDAVG_BALANCE");
     const int bal = env ? std::atoi(env) : FEDAVG_BALANCE_DEFAULT;
+    // FEDAVG_BALANCE_ALWAYS=1: the balanced orders for every layout (A/B and the geometry tests)
+    const char* always_env = std::getenv("FEDAVG_BALANCE_ALWAYS");
+    const bool always = always_env && std::atoi(always_env) != 0;
     int cus = 0;
     if (bal && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
       int per_cu = 0;
+      // only where the launch's last wave of workgroups is thin (less than half the resident
+      // slots): elsewhere the plain order's tail already balances and the balanced order's PV
+      // kernel is the slower one (profiles/r03_ab_matrix.txt)
+      auto thin_tail = [&](size_t tiles, int64_t slots) {
+        const int64_t rem = static_cast<int64_t>(tiles) % slots;
+        return always || (tiles > static_cast<size_t>(slots) && rem > 0 && 2 * rem < slots);
+      };
       if ((bal & 1) && kTileWide > 0 &&
           hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA, kTileWide>),
-              Geo<float, 1, kTileWide>::THREADS, 0) == hipSuccess && per_cu > 0)
+              &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA, kTileWide, true>),
+              Geo<float, 1, kTileWide>::THREADS, 0) == hipSuccess && per_cu > 0 &&
+          thin_tail(c->tilesw.size(), static_cast<int64_t>(per_cu) * cus))
         c->tilesw_bal_head =
             build_balanced_tiles(c->seg_numel, kTileWide, Geo<float, 1, kTileWide>::LANES * Vec16<float>::n,
                                  static_cast<int64_t>(per_cu) * cus, c->tilesw_bal);
       per_cu = 0;
       if ((bal & 2) &&
           hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<double, OUT_F32, 1, true, FOLD_FMA, kTile1>),
-              Geo<double, 1, kTile1>::THREADS, 0) == hipSuccess && per_cu > 0)
+              &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<double, OUT_F32, 1, true, FOLD_FMA, kTile1, true>),
+              Geo<double, 1, kTile1>::THREADS, 0) == hipSuccess && per_cu > 0 &&
+          thin_tail(c->tiles1.size(), static_cast<int64_t>(per_cu) * cus))
         c->tiles1_bal_head =
             build_balanced_tiles(c->seg_numel, kTile1, Geo<double, 1, kTile1>::LANES * Vec16<double>::n,
                                  static_cast<int64_t>(per_cu) * cus, c->tiles1_bal);
@@ -2495,6 +2723,8 @@ int32_t fedavg_find_nan_clients(fedavg_ctx* c, const void* const* client_ptrs, i
     switch (in_dtype) {
       case FEDAVG_QSGD_F32: hipLaunchKernelGGL(qsgd_nan_scan_kernel<float>, grid, dim3(kThreads), 0, s, c->d_tiles1, c->d_segs, tab, K, d_bad); break;
       case FEDAVG_QSGD_F64: hipLaunchKernelGGL(qsgd_nan_scan_kernel<double>, grid, dim3(kThreads), 0, s, c->d_tiles1, c->d_segs, tab, K, d_bad); break;
+      case FEDAVG_NNADQ_F32: hipLaunchKernelGGL(nnadq_nan_scan_kernel<float>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
+      case FEDAVG_NNADQ_F64: hipLaunchKernelGGL(nnadq_nan_scan_kernel<double>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
       case FEDAVG_F32: hipLaunchKernelGGL(nan_scan_kernel<float>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
       case FEDAVG_F16: hipLaunchKernelGGL(nan_scan_kernel<__half>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;
       case FEDAVG_BF16: hipLaunchKernelGGL(nan_scan_kernel<bf16_t>, grid, dim3(kThreads), 0, s, c->d_tiles1, tab, K, d_bad); break;

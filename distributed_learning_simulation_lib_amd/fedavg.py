@@ -103,10 +103,11 @@ def _stream_handle(device: torch.device) -> ctypes.c_void_p:
 
 def dtype_code(dtype) -> int:
     """C-ABI input format of a torch dtype, or of a quantised record format
-    (``quantized.QSGD_F32`` / ``QSGD_F64``, which carry their own code)."""
+    (``quantized.QSGD_F32`` / ``QSGD_F64`` / ``NNADQ_F32`` / ``NNADQ_F64``, which carry their
+    own code)."""
     if not isinstance(dtype, torch.dtype):
         code = getattr(dtype, "code", None)
-        if code in (_native.QSGD_F32, _native.QSGD_F64):
+        if code in _native.RECORD_CODES:
             return int(code)
         raise TypeError(f"no HIP FedAvg kernel for input format {dtype}")
     try:
@@ -392,10 +393,12 @@ class FedAvgContext:
             raise ValueError("client table does not match the layout")
         code = dtype_code(in_dtype)
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        if code in (_native.QSGD_F32, _native.QSGD_F64):
-            # one uint8 record per tensor (include/fedavg_hip.h record layout)
-            need = [int(self._lib.fedavg_qsgd_record_bytes(n)) for n in self.layout.numels]
-            table.validate(need, 1, dev, ("qsgd", tuple(need), dev))
+        if code in _native.RECORD_CODES:
+            # one uint8 record per tensor (include/fedavg_hip.h record layouts)
+            nbytes = (self._lib.fedavg_qsgd_record_bytes if code in (_native.QSGD_F32, _native.QSGD_F64)
+                      else self._lib.fedavg_nnadq_record_bytes)
+            need = [int(nbytes(n)) for n in self.layout.numels]
+            table.validate(need, 1, dev, ("record", tuple(need), dev))
         else:
             esize = torch.empty((), dtype=in_dtype).element_size()
             table.validate(self.layout.numels, esize, dev, (in_dtype, tuple(self.layout.numels), dev))

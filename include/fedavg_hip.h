@@ -71,6 +71,17 @@ enum fedavg_dtype {
    * ones; split policies do not apply. */
   FEDAVG_QSGD_F32 = 4,
   FEDAVG_QSGD_F64 = 5,
+  /* NNADQ records (NNADQServerEndpoint, quantized_endpoint.py:114-142, dequantised by
+   * QuantServerEndpoint.get :69-77): a deterministic per-tensor affine code, 16-byte aligned,
+   * fedavg_nnadq_record_bytes(numel) bytes:
+   *   [0, 8)   lo, fp64 (for FEDAVG_NNADQ_F32 an fp32 value held exactly)
+   *   [8, 16)  step, fp64 (likewise)
+   *   [16, 20) levels L, int32 in [1, 255] (codes are in [0, L])
+   *   [32, 32 + numel)  code per element, uint8
+   * The dequantised element is x = code * step + lo (two roundings) in fp32 (NNADQ_F32) or
+   * fp64 (NNADQ_F64), then folded exactly like a dense input. Same entry points as QSGD. */
+  FEDAVG_NNADQ_F32 = 6,
+  FEDAVG_NNADQ_F64 = 7,
 };
 
 /* status codes */
@@ -108,7 +119,8 @@ int32_t fedavg_build_flags(void);
  * d in {f32, f16, bf16, f64}: "ae_<d>", "lanes_<d>" (elements per lane / lanes per tile of the
  * whole-layout table), "ae4096_<d>", "lanes4096_<d>" (the 4096-element table), "group_<d>"
  * (clients loaded per group), "pipe_<d>" (clients per pipeline stage, 0 = no pipeline);
- * "qsgd_tile", "qsgd_ae", "qsgd_group"; "pers_chunk", "pers_jb" (receivers per wave),
+ * "qsgd_tile", "qsgd_ae", "qsgd_group"; "nnadq_tile", "nnadq_ae", "nnadq_group",
+ * "nnadq_header"; "pers_chunk", "pers_jb" (receivers per wave),
  * "pers_group" (receivers per launch), "pers_u", "pers_ring_stage", "pers_ring_depth".
  * FEDAVG_ERR_INVALID for an unknown name. */
 int32_t fedavg_kernel_constant(const char* name, int64_t* out);
@@ -117,6 +129,9 @@ int32_t fedavg_kernel_constant(const char* name, int64_t* out);
  * (see FEDAVG_QSGD_F32). Pure functions; -1 for numel < 0. */
 int64_t fedavg_qsgd_record_bytes(int64_t numel);
 int64_t fedavg_qsgd_sign_offset(int64_t numel);
+/* Byte size of one NNADQ record of a numel-element tensor (see FEDAVG_NNADQ_F32); -1 for
+ * numel < 0. */
+int64_t fedavg_nnadq_record_bytes(int64_t numel);
 const char* fedavg_last_error(void);
 
 /*

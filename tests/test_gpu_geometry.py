@@ -104,7 +104,12 @@ def _run(ctx, tabs, dt, out_dtype, device, base_dev=None):
 
 @pytest.mark.parametrize("d", list(DT))
 @pytest.mark.parametrize("fold", ["float", "int", "delta"])
-def test_fedavg_kernel_edges_bit_identical(hip_device, d, fold):
+@pytest.mark.parametrize("balance", ["auto", "always"])
+def test_fedavg_kernel_edges_bit_identical(hip_device, d, fold, balance, monkeypatch):
+    # "always": the balanced whole-layout orders (pieces of whole lane-vectors, the PV kernels)
+    # for every layout, not only where the last wave of workgroups is thin
+    if balance == "always":
+        monkeypatch.setenv("FEDAVG_BALANCE_ALWAYS", "1")
     dt = DT[d]
     lengths = fedavg_lengths(d)
     layout = ModelLayout(names=tuple(f"t{i}" for i in range(len(lengths))), shapes=tuple((m,) for m in lengths))
@@ -128,8 +133,9 @@ def test_fedavg_kernel_edges_bit_identical(hip_device, d, fold):
 
 
 @pytest.mark.parametrize("d", ["f32", "f64"])
-def test_fedavg_balanced_head_bit_identical(hip_device, d):
+def test_fedavg_balanced_head_bit_identical(hip_device, d, monkeypatch):
     """A layout of many whole tiles: the balanced order's head of whole waves, then the pieces."""
+    monkeypatch.setenv("FEDAVG_BALANCE_ALWAYS", "1")
     dt = DT[d]
     tile = K("tile_wide") if d == "f32" else K("tile")
     lengths = [700 * tile + 777, 3 * tile, 1]

@@ -470,14 +470,20 @@ def main_personalized(args: argparse.Namespace) -> int:
     return 0
 
 
-def make_qsgd_clients(layout: ModelLayout, n: int, device: torch.device, level: int = 255):
-    """n synthetic QSGD-quantised clients (fp32 codec), records resident in HBM: each client's
-    x ~ N(0,1) (seeded per client) quantised with the client-side quantiser
-    (quantized.quantize_tensor, level 255) — the byte stream a StochasticQuantClientEndpoint
-    worker sends (quantized_endpoint.py:96-99)."""
-    from distributed_learning_simulation_lib_amd.quantized import quantize_tensor, record_bytes
+def make_qsgd_clients(layout: ModelLayout, n: int, device: torch.device, level: int = 255, scheme: str = "qsgd"):
+    """n synthetic quantised clients (fp32 codec), records resident in HBM: each client's
+    x ~ N(0,1) (seeded per client) quantised with the client-side quantiser — QSGD
+    (quantized.quantize_tensor, level 255: what a StochasticQuantClientEndpoint worker sends,
+    quantized_endpoint.py:96-99) or NNADQ (quantized.nnadq_quantize_tensor, weight 0.01: an
+    NNADQClientEndpoint worker, :114-124)."""
+    from distributed_learning_simulation_lib_amd.quantized import (
+        NNADQ_F32,
+        nnadq_quantize_tensor,
+        quantize_tensor,
+        record_bytes,
+    )
 
-    sizes = [record_bytes(m) for m in layout.numels]
+    sizes = [NNADQ_F32.record_bytes(m) if scheme == "nnadq" else record_bytes(m) for m in layout.numels]
     offs = np.cumsum([0] + sizes[:-1]).tolist()
     total = sum(sizes)
     buckets = torch.zeros((n, total), dtype=torch.uint8, device=device)
@@ -486,9 +492,13 @@ def make_qsgd_clients(layout: ModelLayout, n: int, device: torch.device, level: 
         g.manual_seed(1234 + i)
         for o, m, sz in zip(offs, layout.numels, sizes):
             x = torch.randn(m, generator=g, device=device)
-            buckets[i, o : o + sz] = quantize_tensor(x, level, generator=g).record
+            q = nnadq_quantize_tensor(x, NNADQ_WEIGHT) if scheme == "nnadq" else quantize_tensor(x, level, generator=g)
+            buckets[i, o : o + sz] = q.record
     views = [[buckets[i, o : o + sz] for o, sz in zip(offs, sizes)] for i in range(n)]
     return buckets, views, total
+
+
+NNADQ_WEIGHT = 0.01
 
 
 def cpu_baseline_qsgd(layout: ModelLayout, budget_s: float = 12.0, sample_clients: int = 4) -> dict:
@@ -541,18 +551,65 @@ def cpu_baseline_qsgd(layout: ModelLayout, budget_s: float = 12.0, sample_client
     }
 
 
+def cpu_baseline_nnadq(layout: ModelLayout, budget_s: float = 12.0, sample_clients: int = 4) -> dict:
+    """The reference's server path for NNADQ updates on the host: QuantServerEndpoint.get
+    dequantises every tensor (x = code * step + lo in torch CPU ops, quantized_endpoint.py:69-77,
+    127-136), then FedAVGAlgorithm's op sequence (oracle/ref_torch_cpu.py)."""
+    sys.path.insert(0, str(REPO))
+    from oracle.ref_torch_cpu import RefOpsFedAvg
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    weights = dataset_size_weights(sample_clients)
+    g = torch.Generator().manual_seed(1234)
+    clients = []
+    for _ in range(sample_clients):
+        c = {}
+        for name, shape in zip(layout.names, layout.shapes):
+            m = int(np.prod(shape))
+            c[name] = (torch.rand((), generator=g).item() - 0.5, torch.rand((), generator=g).item() * 1e-2,
+                       torch.randint(0, 201, (m,), generator=g, dtype=torch.uint8), shape)
+        clients.append(c)
+    nbytes = sample_clients * sum(32 + m for m in layout.numels) + layout.total_numel * 4
+    times = []
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < budget_s and len(times) < 1000:
+        algo = RefOpsFedAvg()
+        t0 = time.perf_counter()
+        for c, w in zip(clients, weights):
+            dense = {name: (codes.to(torch.float32) * step + lo).view(shape)
+                     for name, (lo, step, codes, shape) in c.items()}
+            algo.add(dense, w)
+        out = {k: v.to(torch.float32) for k, v in algo.finish().items()}
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {
+        "value": round(nbytes / best / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (
+            f"{sample_clients} NNADQ-quantised clients x ResNet-18 layout (fp32 codec): host dequantisation "
+            f"(code * step + lo) + the reference FedAvg op sequence in torch CPU, best of {len(times)} runs "
+            f"over {time.perf_counter() - t_start:.1f} s"
+        ),
+    }
+
+
 def main_qsgd(args: argparse.Namespace) -> int:
     """--workload qsgd: one FedAvg round over QSGD-quantised client updates (the server behind
     StochasticQuantServerEndpoint, quantized_endpoint.py:102-111) with the dequantisation fused
     into the fold; records resident in HBM, one GPU."""
-    from distributed_learning_simulation_lib_amd.quantized import QSGD_F32
+    from distributed_learning_simulation_lib_amd.quantized import NNADQ_F32, QSGD_F32
 
+    nnadq = args.workload == "nnadq"
+    fmt = NNADQ_F32 if nnadq else QSGD_F32
     device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(device)
     layout = LAYOUTS[args.layout]()
     P, T, N = layout.total_numel, layout.num_segments, args.clients_per_gpu
     out_dtype = getattr(torch, args.out_dtype)
-    buckets, views, client_bytes = make_qsgd_clients(layout, N, device)
+    buckets, views, client_bytes = make_qsgd_clients(layout, N, device, scheme="nnadq" if nnadq else "qsgd")
     weights = dataset_size_weights(N)
     table = ClientTable(T)
     for row, w in zip(views, weights):
@@ -561,7 +618,7 @@ def main_qsgd(args: argparse.Namespace) -> int:
     offs, padded = layout.padded_offsets(torch.empty((), dtype=out_dtype).element_size())
     out_flat = torch.empty(padded, dtype=out_dtype, device=device)
     outs = OutputTable([out_flat[o : o + m] for o, m in zip(offs, layout.numels)], layout, device, out_dtype)
-    plan = ctx.plan(table, QSGD_F32, outs, out_dtype)
+    plan = ctx.plan(table, fmt, outs, out_dtype)
 
     def step() -> None:
         plan.run()
@@ -590,9 +647,10 @@ def main_qsgd(args: argparse.Namespace) -> int:
     if not args.no_cpu_baseline:
         del buckets, views, table, plan
         torch.cuda.empty_cache()
-        cpu = cpu_baseline_qsgd(layout)
+        cpu = cpu_baseline_nnadq(layout) if nnadq else cpu_baseline_qsgd(layout)
     line = {
-        "metric": "aggregated GB/s (device-resident), N-client weighted FedAvg reduce over QSGD-quantised updates",
+        "metric": ("aggregated GB/s (device-resident), N-client weighted FedAvg reduce over "
+                   f"{'NNADQ' if nnadq else 'QSGD'}-quantised updates"),
         "value": round(job_bytes / step_s / 1e9, 2),
         "unit": "GB/s",
         "n_gpus": 1,
@@ -604,9 +662,12 @@ def main_qsgd(args: argparse.Namespace) -> int:
         "vs_baseline": None,
         "client_elements_per_s": round(N * P / step_s, 1),
         "dtype": "f64",
-        "data": "synthetic: x ~ N(0,1) per client, QSGD-quantised on the GPU (inf-norm, level 255, stochastic rounding); dataset-size weights",
-        "config": {"workload": f"fedavg_qsgd255_{args.layout}_{N}_clients", "clients": N, "params_per_client": P,
-                   "tensors_per_client": T, "record_bytes_per_client": client_bytes, "codec": "qsgd_f32 (level 255)",
+        "data": ("synthetic: x ~ N(0,1) per client, " + (
+            f"NNADQ-quantised on the GPU (deterministic, weight {NNADQ_WEIGHT})" if nnadq else
+            "QSGD-quantised on the GPU (inf-norm, level 255, stochastic rounding)") + "; dataset-size weights"),
+        "config": {"workload": f"fedavg_{'nnadq' if nnadq else 'qsgd255'}_{args.layout}_{N}_clients", "clients": N,
+                   "params_per_client": P, "tensors_per_client": T, "record_bytes_per_client": client_bytes,
+                   "codec": "nnadq_f32" if nnadq else "qsgd_f32 (level 255)",
                    "accumulate_dtype": "float64", "out_dtype": args.out_dtype},
         "roofline": {
             "bound": "hbm",
@@ -615,7 +676,8 @@ def main_qsgd(args: argparse.Namespace) -> int:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None,
-            "kernel": f"qsgd_tile_kernel<OUT_{'F32' if out_dtype == torch.float32 else 'F64'}, float, true>",
+            "kernel": (f"{'nnadq' if nnadq else 'qsgd'}_tile_kernel<OUT_{'F32' if out_dtype == torch.float32 else 'F64'}, "
+                       f"float{', fma' if nnadq else ''}, true>"),
             "bytes_per_launch": job_bytes,
             "mean_launch_ms": round(per_launch_s * 1e3, 4),
             "launches": launches,
@@ -973,9 +1035,9 @@ def main() -> int:
     ap.add_argument("--no-plan", action="store_true", help="re-stage the client table every round")
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run the sharded path (partial + RCCL reduce + finalize) anyway")
-    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd", "plugin", "gradient"],
+    ap.add_argument("--workload", default="fedavg", choices=["fedavg", "personalized", "qsgd", "nnadq", "plugin", "gradient"],
                     help="fedavg: the headline reduce; personalized: PersonalizedFedAVG (one GPU); "
-                         "qsgd: FedAvg over QSGD-quantised updates, dequantisation fused (one GPU); "
+                         "qsgd / nnadq: FedAvg over QSGD- / NNADQ-quantised updates, dequantisation fused (one GPU); "
                          "plugin: the headline round through FedAVGAlgorithm's plugin calls (one GPU); "
                          "gradient: GradientWorker's in-round rounds through the plugin, as a latency "
                          "(--clients-per-gpu default 8)")
@@ -996,7 +1058,7 @@ def main() -> int:
         return main_dry(args)
     if args.workload == "personalized":
         return main_personalized(args)
-    if args.workload == "qsgd":
+    if args.workload in ("qsgd", "nnadq"):
         return main_qsgd(args)
     if args.workload in ("plugin", "gradient"):
         return main_plugin(args)

@@ -208,6 +208,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // 16-byte vector of the input type
 template <typename T>
@@ -861,14 +862,24 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
 #ifndef FEDAVG_QSGD_ABLATE
 #define FEDAVG_QSGD_ABLATE 0
 #endif
-#ifndef FEDAVG_QSGD_GROUP
-#define FEDAVG_QSGD_GROUP 4
+#ifndef FEDAVG_QSGD_AE
+#define FEDAVG_QSGD_AE 16  // elements per lane: 16 (256-lane workgroups) or 8 (512 lanes)
 #endif
+static_assert(FEDAVG_QSGD_AE == 16 || FEDAVG_QSGD_AE == 8, "QSGD lanes hold 16 or 8 elements");
+// one wave of the workgroup DMAs each client table of a group: clients per group = waves
+#define FEDAVG_QSGD_GROUP (4096 / FEDAVG_QSGD_AE / 64)
 constexpr int kQsgdGroup = FEDAVG_QSGD_GROUP;
-static_assert(FEDAVG_QSGD_GROUP == 4, "one wave of the 256-lane workgroup DMAs each client table of a group");
+#ifndef FEDAVG_QSGD_DEPTH
+#define FEDAVG_QSGD_DEPTH 1
+#endif
+// groups whose loads are in flight while a group folds; DEPTH + 1 LDS table buffers
+constexpr int kQsgdDepth = FEDAVG_QSGD_DEPTH;
+constexpr int kQsgdBufs = kQsgdDepth + 1;
+static_assert(kQsgdDepth >= 1 && kQsgdDepth <= 3, "QSGD prefetch depth 1..3");
+
 constexpr int kQsgdTable = 256;  // entries per client (|p| per slot value)
-constexpr int kQsgdLanes = 256;
-constexpr int kQsgdAE = 16;
+constexpr int kQsgdAE = FEDAVG_QSGD_AE;
+constexpr int kQsgdLanes = 4096 / kQsgdAE;
 
 template <typename DQ>
 __device__ __forceinline__ double qsgd_product(double norm, int level, int slot, double w) {
@@ -898,7 +909,13 @@ __global__ __launch_bounds__(kQsgdTable) void qsgd_table_kernel(CallTables tab, 
   const int level = to_const<int32_t>(rec)[2];
   const double w = to_const<double>(tab.w)[row];
   const int s = static_cast<int>(threadIdx.x);
-  qtab[row * kQsgdTable + s] = __builtin_fabs(qsgd_product<DQ>(norm, level, s, w));
+  const double p = __builtin_fabs(qsgd_product<DQ>(norm, level, s, w));
+  // entry 0 is a zero (or a NaN, for a non-finite norm / weight): its sign bit carries the
+  // client's product sign, signbit(norm) ^ signbit(w), which the fold reads with one broadcast
+  // LDS load instead of keeping norm and weight in SGPRs (the fold inserts every element's sign
+  // itself, so entry 0's magnitude is all the fold takes from it)
+  const bool flip = __builtin_signbit(norm) != __builtin_signbit(w);
+  qtab[row * kQsgdTable + s] = (s == 0 && flip) ? -p : p;
 }
 
 __device__ __forceinline__ void wait_vmcnt0() {
@@ -996,9 +1013,27 @@ __device__ __forceinline__ void record_tile_finish(const KArgs& a, const TileDes
   }
 }
 
+// f(integral_constant<int, I>) for I in [I0, N), unrolled at compile time
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void qsgd_wait_vmcnt() {
+  // s_waitcnt vmcnt(N) (bits 3:0 and 15:14; expcnt / lgkmcnt: no wait)
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 template <int OUT, typename DQ, bool FULL, bool VEC>
 __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable]) {
   constexpr int AE = kQsgdAE;
+  constexpr int G = kQsgdGroup;
+  constexpr int D = kQsgdDepth;
+  constexpr int NB = kQsgdBufs;
   const int seg = td.seg;
   const int count = td.count;
   const int li = static_cast<int>(threadIdx.x);
@@ -1007,47 +1042,47 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
 
   const int kseg = to_const<int32_t>(a.tab.kseg)[seg];
   const kptr<uint64_t> cp = to_const<uint64_t>(a.tab.cptrs) + static_cast<int64_t>(seg) * a.K;
-  const kptr<double> wp = to_const<double>(a.tab.w) + static_cast<int64_t>(seg) * a.K;
   const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;
   const int64_t numel = to_const<int64_t>(a.segs)[2 * seg + 1];
-  const int64_t slot_off = 16 + td.start + e0;
-  const int64_t sign_off = 16 + ((numel + 15) & ~int64_t(15)) + (td.start + e0) / 8;
+  // a lane past the tile's end loads from the record's start instead (in bounds; its sums are
+  // never stored), so every wave issues the same vector memory operations per group and the
+  // counted waits below hold for every wave
+  const int64_t slot_off = lane_live ? 16 + td.start + e0 : 0;
+  const int64_t sign_off = lane_live ? 16 + ((numel + 15) & ~int64_t(15)) + (td.start + e0) / 8 : 0;
 
   double acc[AE];
   bool have = record_tile_acc_in<FULL, AE>(a, seg, acc_base, e0, count, acc);
 
-  // Client loads of one group (slots + sign words), issued one group ahead of its fold so the
-  // HBM latency of group g+1 hides under the fold of group g. The group's |product| tables
-  // (built once per call by qsgd_table_kernel) go global -> LDS by DMA in the same step: wave w
-  // moves client k + w's 2 KiB table (two 1-KiB global_load_lds_dwordx4), the last client again
-  // for a short group, so every wave issues the same two DMAs.
+  // Client loads of one group (slots + sign words) and its G |product| tables (global -> LDS
+  // by DMA: wave w moves client k + w's 2 KiB table in two 1-KiB global_load_lds_dwordx4, the
+  // last client again for a short group), issued D groups ahead of the group's fold into one of
+  // D + 1 LDS buffers: every wave issues exactly kOps vector memory operations per group, so
+  // "the group D - 1 issues back has landed" is a counted vmcnt.
+  constexpr int kOps = 2 * G + 2;
+  using SlotVec = typename std::conditional<AE == 16, u32x4, u32x2>::type;  // AE slot bytes
   struct GroupRegs {
-    u32x4 slots[kQsgdGroup];
-    uint32_t signs[kQsgdGroup];
-    double nrm[kQsgdGroup], wk[kQsgdGroup];  // wave-uniform (SGPRs): record header, weight
+    SlotVec slots[G];
+    uint32_t signs[G];  // AE sign bits (16-bit / 8-bit load)
   };
   const int wave = __builtin_amdgcn_readfirstlane(li >> 6);
   const int lane = li & 63;
   const double* const tabs = a.qtab + static_cast<int64_t>(seg) * a.K * kQsgdTable;
   auto issue = [&](GroupRegs& r, int buf, int k) {
-    const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
+    const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
-    for (int c = 0; c < kQsgdGroup; ++c) {
+    for (int c = 0; c < G; ++c) {
       const int kc = k + min(c, n - 1);
-      const uint64_t rec = cp[kc];
-      r.nrm[c] = to_const<double>(reinterpret_cast<const void*>(rec))[0];
-      r.wk[c] = wp[kc];
-      if (lane_live) {
-        const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(cp[kc]));
-#if FEDAVG_NT
-        r.slots[c] = __builtin_nontemporal_load((gptr<const u32x4>)(rp + slot_off));
-#else
-        r.slots[c] = *(gptr<const u32x4>)(rp + slot_off);
-#endif
-        r.signs[c] = *(gptr<const uint16_t>)(rp + sign_off);
+      const uint64_t rp = cp[kc];
+      // inline-asm loads: the compiler does not track them, so it inserts no waits of its own
+      // (its loop-carried tracking otherwise drains vmcnt to 0 between groups); the counted wait
+      // at the top of each step covers every use, and no register of a pending load is reused
+      // before that use (the value is live from here to the fold)
+      if constexpr (AE == 16) {
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r.slots[c]) : "v"(rp + slot_off) : "memory");
+        asm volatile("global_load_ushort %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
       } else {
-        r.slots[c] = u32x4{0u, 0u, 0u, 0u};
-        r.signs[c] = 0xffffu;
+        asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(r.slots[c]) : "v"(rp + slot_off) : "memory");
+        asm volatile("global_load_ubyte %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
       }
     }
     const double* src = tabs + static_cast<int64_t>(k + min(wave, n - 1)) * kQsgdTable;
@@ -1060,17 +1095,19 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   // Fold of one group from LDS buffer B (compile-time, so every table read is
   // `ds_read_b64 v, v_off offset:<buffer base>`). The table holds |p|; the sign of each
   // product is sign(x_hat) ^ sign(w) = (element negative) ^ signbit(norm) ^ signbit(w)
-  // (every step of the dequantisation and the product is sign-symmetric, zeros included),
+  // (every step of the dequantisation and the product is sign-symmetric, zeros included) —
+  // the client's signbit(norm) ^ signbit(w) is entry 0's sign bit (qsgd_table_kernel) — and is
   // inserted into the high word with one bit-field insert.
   auto run = [&](auto buf_tag, const GroupRegs& r, int k) {
     constexpr int B = decltype(buf_tag)::value;
-    const int n = min(kQsgdGroup, kseg - k);  // wave-uniform
+    const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
-    for (int c = 0; c < kQsgdGroup; ++c) {
+    for (int c = 0; c < G; ++c) {
       if (c < n) {
-        const bool flip = __builtin_signbit(r.nrm[c]) != __builtin_signbit(r.wk[c]);  // wave-uniform
-        const uint32_t neg = flip ? r.signs[c] : ~r.signs[c];  // per element: 1 = negative product
         const char* tab = reinterpret_cast<const char*>(lut[B][c]);
+        const int32_t t0hi = reinterpret_cast<const int32_t*>(tab)[1];  // broadcast read
+        // per element: 1 = negative product
+        const uint32_t neg = r.signs[c] ^ ~static_cast<uint32_t>(t0hi >> 31);
         // all 16 table reads of this client in flight before the first add (the compiler
         // otherwise keeps ~4 outstanding and waits on each batch)
         double pav[AE];
@@ -1090,7 +1127,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
 #pragma unroll
         for (int j = 0; j < AE; ++j) {
           // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte of
-          // the little-endian 16-bit sign word, element j >= 8 bit 15 - (j - 8)
+          // the little-endian sign word, element j >= 8 bit 15 - (j - 8)
           const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
           const uint32_t sb = neg << (31 - bit);
           const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pav[j]));
@@ -1101,27 +1138,36 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
       }
     }
   };
-  // Two groups per iteration (LDS buffers 0 / 1). At the top of each step a wave waits for
-  // everything it issued (the group's loads and table DMAs), and the barrier publishes every
-  // wave's DMAs; only then is the next group issued into the other buffer, which the barrier
-  // also proves every wave has finished reading (its fold was two steps back).
-  GroupRegs r0, r1;
-  if (kseg > 0) issue(r0, 0, 0);
-  for (int k = 0; k < kseg; k += 2 * kQsgdGroup) {
-    const bool second = k + kQsgdGroup < kseg;
-    wait_vmcnt0();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (second) issue(r1, 1, k + kQsgdGroup);
-    run(std::integral_constant<int, 0>{}, r0, k);
-    if (second) {
-      wait_vmcnt0();
+  // Group i folds from buffer i % NB. At the top of each step a wave waits until its loads and
+  // DMAs of that group landed (the groups issued after it may stay in flight), and the barrier
+  // publishes every wave's DMAs; only then is group i + D issued, into buffer (i + D) % NB —
+  // the buffer of group i - 1, which the barrier proves every wave has finished reading.
+  GroupRegs r[NB];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (kseg > 0) issue(r[d], d, min(d * G, (kseg - 1) / G * G));
+  for (int k = 0; k < kseg; k += NB * G) {
+    bool go = true;
+    static_for<0, NB>([&](auto b_tag) {
+      constexpr int b = decltype(b_tag)::value;
+      const int kk = k + b * G;
+      if (!go || kk >= kseg) {  // wave-uniform
+        go = false;
+        return;
+      }
+      // D - 1 groups were issued after group kk (past the last group the issue repeats the last
+      // group: L2 hits into a buffer nobody reads, so every step's count is the same)
+      __builtin_amdgcn_sched_barrier(0);
+      qsgd_wait_vmcnt<(D - 1) * kOps>();
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (k + 2 * kQsgdGroup < kseg) issue(r0, 0, k + 2 * kQsgdGroup);
-      run(std::integral_constant<int, 1>{}, r1, k + kQsgdGroup);
-    }
+      issue(r[(b + D) % NB], (b + D) % NB, min(kk + D * G, (kseg - 1) / G * G));
+      run(b_tag, r[b], kk);
+    });
   }
+  // the repeated issues past the last group are still in flight: no DMA may land in LDS after
+  // the workgroup has left it
+  qsgd_wait_vmcnt<0>();
   have = have || (kseg > 0);
   if (!have) return;
   record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
@@ -1129,7 +1175,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
 
 template <int OUT, typename DQ, bool VEC>
 __global__ __launch_bounds__(kQsgdLanes) void qsgd_tile_kernel(KArgs a) {
-  __shared__ double lut[2][kQsgdGroup][kQsgdTable];
+  __shared__ double lut[kQsgdBufs][kQsgdGroup][kQsgdTable];
   const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
   if (td.count == kTile1) {
     qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut);
@@ -1184,9 +1230,12 @@ constexpr int kNnadqHeader = 32;
 constexpr int kNnadqLanes = 256;
 constexpr int kNnadqAE = 16;
 #ifndef FEDAVG_NNADQ_GROUP
-#define FEDAVG_NNADQ_GROUP 8
+#define FEDAVG_NNADQ_GROUP 4
 #endif
 constexpr int kNnadqGroup = FEDAVG_NNADQ_GROUP;
+#ifndef FEDAVG_NNADQ_PK
+#define FEDAVG_NNADQ_PK 0  // 1: packed fp32 dequantisation (v_pk_mul_f32 / v_pk_add_f32; measured slower)
+#endif
 static_assert(kNnadqLanes * kNnadqAE == kTile1, "NNADQ launches walk the 4096-element tile table");
 
 template <typename DQ>
@@ -1249,6 +1298,24 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c < n) {
+#if FEDAVG_NNADQ_PK
+        if constexpr (std::is_same<DQ, float>::value) {
+          // fp32 codec: two elements per v_pk_mul_f32 / v_pk_add_f32 (each lane of the pair
+          // rounds on its own, exactly as the scalar code * step, + lo)
+          const f32x2 st2 = {r.step[c], r.step[c]};
+          const f32x2 lo2 = {r.lo[c], r.lo[c]};
+#pragma unroll
+          for (int j = 0; j < AE; j += 2) {
+            const uint32_t word = r.codes[c][j >> 2];
+            const f32x2 cc = {static_cast<float>((word >> (8 * (j & 3))) & 0xffu),
+                              static_cast<float>((word >> (8 * ((j + 1) & 3))) & 0xffu)};
+            const f32x2 v = cc * st2 + lo2;
+            acc[j] = fold<FOLD>(acc[j], static_cast<double>(v.x), r.wk[c], 0.0);
+            acc[j + 1] = fold<FOLD>(acc[j + 1], static_cast<double>(v.y), r.wk[c], 0.0);
+          }
+          continue;
+        }
+#endif
 #pragma unroll
         for (int j = 0; j < AE; ++j) {
           const uint32_t code = (r.codes[c][j >> 2] >> (8 * (j & 3))) & 0xffu;

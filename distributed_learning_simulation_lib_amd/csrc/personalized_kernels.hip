@@ -91,6 +91,9 @@ constexpr int kU = PERS_U;             // clients loaded ahead per lane
 #ifndef PERS_RING_MULADD  // 1: the mul + add fold (float weights) streams through the ring as well
 #define PERS_RING_MULADD 0
 #endif
+#ifndef PERS_PREFETCH  // 1: the ring loop loads client k + 1's weight row (and ring slice) under client k's folds
+#define PERS_PREFETCH 0
+#endif
 
 struct PChunk {
   int32_t seg;
@@ -365,6 +368,16 @@ struct Glds<float> {
     x[2] = v.z;
     x[3] = v.w;
   }
+  using RawT = f32x4;  // the slice as read (widened only where it is folded)
+  __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
+    return *reinterpret_cast<const f32x4*>(slot + lane * 16);
+  }
+  __device__ __forceinline__ static void expand(const RawT& v, double* x) {
+    x[0] = v.x;
+    x[1] = v.y;
+    x[2] = v.z;
+    x[3] = v.w;
+  }
 };
 template <>
 struct Glds<double> {
@@ -384,6 +397,16 @@ struct Glds<double> {
     x[1] = lo.y;
     x[2] = hi.x;
     x[3] = hi.y;
+  }
+  using RawT = f64x2x2;
+  __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
+    return RawT{*reinterpret_cast<const f64x2*>(slot + lane * 16), *reinterpret_cast<const f64x2*>(slot + 1024 + lane * 16)};
+  }
+  __device__ __forceinline__ static void expand(const RawT& v, double* x) {
+    x[0] = v.lo.x;
+    x[1] = v.lo.y;
+    x[2] = v.hi.x;
+    x[3] = v.hi.y;
   }
 };
 template <typename T>
@@ -428,6 +451,51 @@ __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, in
 #endif
   };
   for (int st = 0; st < kD && st < nst; ++st) issue(st);
+#if PERS_PREFETCH && !PERS_RING_WEIGHTS
+  // Software pipeline, one client ahead: client k + 1's weight row (SGPRs, s_load from L2) and
+  // — inside a stage — its ring slice (ds_read) are issued before client k's 64 folds, and one
+  // explicit lgkmcnt(0) after the folds retires both (the compiler would otherwise wait for the
+  // weights right after issuing them: SMEM returns out of order, so any LDS wait is lgkmcnt(0)).
+  double wc[kJB], wn[kJB];
+#pragma unroll
+  for (int j = 0; j < kJB; ++j) wc[j] = wt[j];
+  typename G::RawT rc, rn;
+  for (int st = 0; st < nst; ++st) {
+    if (st + kD < nst) issue(st + kD);
+    const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;
+    wait_vmcnt(ahead * (per * G::kIPC + kWIPS));
+    __builtin_amdgcn_s_barrier();
+    const char* stage = ring + (st % kRS) * (kSC * G::kSlice);
+    rc = G::read_raw(stage, lane);
+    __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));  // lgkmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < kSC; ++c) {
+      const int k = st * kSC + c;
+      const int kn = (k + 1 < a.Npad) ? k + 1 : k;
+      const kp<double> wk = wt + static_cast<int64_t>(kn) * a.wstride;
+      double xc[kVE];
+      G::expand(rc, xc);  // client k's slice: retired by the wait at the end of client k - 1
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < kJB; ++j) wn[j] = wk[j];
+      if (c + 1 < kSC) rn = G::read_raw(stage + (c + 1) * G::kSlice, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < kJB; ++j) {
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) acc[v][j] = pfold<FOLD>(acc[v][j], xc[v], wc[j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));  // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < kJB; ++j) wc[j] = wn[j];
+      if (c + 1 < kSC) rc = rn;
+    }
+  }
+  return;
+#endif
   for (int st = 0; st < nst; ++st) {
     if (st + kD < nst) issue(st + kD);
     const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;  // stages issued after st

@@ -15,8 +15,13 @@ for spec in $AB; do
   wl=${spec%%:*}; vs=${spec#*:}
   for v in ${vs//,/ }; do
     lib=""; [ "$v" != main ] && lib=distributed_learning_simulation_lib_amd/_lib/variants/lib_$v.so
-    FEDAVG_HIP_LIB=$lib timeout -k 10 300 python bench.py --workload $wl --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-probe ${BENCH_ARGS:-} > gpurun_out/abwl/${wl}_${v}_$rep.log 2>&1 || { echo "$wl $v failed rc=$?"; tail -20 gpurun_out/abwl/${wl}_${v}_$rep.log; exit 1; }
-    echo "$wl $v $rep $(tail -1 gpurun_out/abwl/${wl}_${v}_$rep.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); r=d.get("roofline") or {}; print(d["ms_per_step"], r.get("mean_launch_ms", r.get("kernel_ms_per_step")), r.get("achieved"), r.get("frac"))')"
+    case $wl in
+      pers_int) wargs="--workload personalized --pers-weights int";;
+      pers_float) wargs="--workload personalized --pers-weights float";;
+      *) wargs="--workload $wl";;
+    esac
+    FEDAVG_HIP_LIB=$lib timeout -k 10 300 python bench.py $wargs --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-probe ${BENCH_ARGS:-} > gpurun_out/abwl/${wl}_${v}_$rep.log 2>&1 || { echo "$wl $v failed rc=$?"; tail -20 gpurun_out/abwl/${wl}_${v}_$rep.log; exit 1; }
+    echo "$wl $v $rep $(tail -1 gpurun_out/abwl/${wl}_${v}_$rep.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); r=d.get("roofline") or {}; print(d["ms_per_step"], r.get("mean_launch_ms", r.get("kernel_ms_per_step", d.get("kernel_ms_per_step"))), r.get("achieved"), r.get("frac"))')"
   done
 done
 done

@@ -643,6 +643,11 @@ def main_qsgd(args: argparse.Namespace) -> int:
     per_launch_s = kernel_ms * 1e-3 / max(launches, 1)
     achieved = job_bytes / per_launch_s / 1e9
     probe = None if args.no_probe else hbm_probes(device)
+    traffic, traffic_src = None, None
+    tfile = REPO / "profiles" / f"r03_traffic_{'nnadq' if nnadq else 'qsgd'}.json"  # PMC pass of this line
+    if tfile.exists() and N == 64 and args.layout == "resnet18" and out_dtype == torch.float32:
+        traffic = float(json.loads(tfile.read_text())["hbm_traffic_bytes_per_step"])
+        traffic_src = f"profiles/{tfile.name}"
     cpu = None
     if not args.no_cpu_baseline:
         del buckets, views, table, plan
@@ -675,7 +680,8 @@ def main_qsgd(args: argparse.Namespace) -> int:
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": (f"{'nnadq' if nnadq else 'qsgd'}_tile_kernel<OUT_{'F32' if out_dtype == torch.float32 else 'F64'}, "
                        f"float{', fma' if nnadq else ''}, true>"),
             "bytes_per_launch": job_bytes,

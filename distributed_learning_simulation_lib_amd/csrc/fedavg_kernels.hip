@@ -856,6 +856,9 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
 // [16 li, 16 li + 16) (one 16-B slot load + one 2-B sign load per client; a wave reads 1 KiB of
 // slots contiguously). Clients go in groups of QG: the group's loads are issued, its QG tables
 // are built into one of two LDS buffers, one barrier, then the fold in arrival order.
+#ifndef FEDAVG_QSGD_PIPE  // 1: a client's table reads issued under the previous client's adds
+#define FEDAVG_QSGD_PIPE 0
+#endif
 #ifndef FEDAVG_QSGD_READ_FENCE
 #define FEDAVG_QSGD_READ_FENCE 1
 #endif
@@ -1101,6 +1104,41 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   auto run = [&](auto buf_tag, const GroupRegs& r, int k) {
     constexpr int B = decltype(buf_tag)::value;
     const int n = min(G, kseg - k);  // wave-uniform
+#if FEDAVG_QSGD_PIPE
+    // client c + 1's table reads in flight while client c's products are added (two register
+    // sets of AE doubles)
+    double pv[2][AE];
+    int32_t t0[2];
+    auto reads = [&](int c, double (&pa)[AE], int32_t& t) {
+      const char* tab = reinterpret_cast<const char*>(lut[B][c]);
+      t = reinterpret_cast<const int32_t*>(tab)[1];
+#pragma unroll
+      for (int j = 0; j < AE; ++j) {
+        const uint32_t word = r.slots[c][j >> 2];
+        const uint32_t off = ((word >> (8 * (j & 3))) & 0xffu) << 3;
+        pa[j] = *reinterpret_cast<const double*>(tab + off);
+      }
+    };
+    if (n > 0) reads(0, pv[0], t0[0]);
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c < n) {
+        if (c + 1 < n) reads(c + 1, pv[(c + 1) & 1], t0[(c + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t neg = r.signs[c] ^ ~static_cast<uint32_t>(t0[c & 1] >> 31);
+#pragma unroll
+        for (int j = 0; j < AE; ++j) {
+          const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
+          const uint32_t sb = neg << (31 - bit);
+          const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pv[c & 1][j]));
+          const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
+          const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
+          acc[j] = acc[j] + p;
+        }
+      }
+    }
+    return;
+#endif
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c < n) {
@@ -1230,9 +1268,12 @@ constexpr int kNnadqHeader = 32;
 constexpr int kNnadqLanes = 256;
 constexpr int kNnadqAE = 16;
 #ifndef FEDAVG_NNADQ_GROUP
-#define FEDAVG_NNADQ_GROUP 4
+#define FEDAVG_NNADQ_GROUP 2
 #endif
 constexpr int kNnadqGroup = FEDAVG_NNADQ_GROUP;
+#ifndef FEDAVG_NNADQ_ASM
+#define FEDAVG_NNADQ_ASM 0  // 1: inline-asm code loads + counted vmcnt waits (measured slower)
+#endif
 #ifndef FEDAVG_NNADQ_PK
 #define FEDAVG_NNADQ_PK 0  // 1: packed fp32 dequantisation (v_pk_mul_f32 / v_pk_add_f32; measured slower)
 #endif
@@ -1270,6 +1311,27 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
     DQ lo[G], step[G];  // wave-uniform (SGPRs): record header
     double wk[G];
   };
+#if FEDAVG_NNADQ_ASM
+  // Inline-asm code loads, every wave G of them per group (a short group repeats its last
+  // client, lanes past the tile's end load the record's first bytes): the compiler tracks none
+  // of them, so it inserts no vmcnt(0) between groups (its loop-carried tracking otherwise
+  // drained the next group's loads before every fold, measured by the ISA); the counted waits
+  // in the loop below retire each group right before its fold.
+  const int64_t code_off_any = lane_live ? code_off : 0;
+  auto issue = [&](GroupRegs& r, int k) {
+    const int n = min(G, kseg - k);  // wave-uniform
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      const int kc = k + min(c, n - 1);
+      const uint64_t rec = cp[kc];
+      const kptr<double> hdr = to_const<double>(reinterpret_cast<const void*>(rec));
+      r.lo[c] = static_cast<DQ>(hdr[0]);
+      r.step[c] = static_cast<DQ>(hdr[1]);
+      r.wk[c] = wp[kc];
+      asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r.codes[c]) : "v"(rec + code_off_any) : "memory");
+    }
+  };
+#else
   auto issue = [&](GroupRegs& r, int k) {
     const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
@@ -1293,6 +1355,7 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
       }
     }
   };
+#endif
   auto run = [&](const GroupRegs& r, int k) {
     const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
@@ -1326,6 +1389,31 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
   };
   GroupRegs r0, r1;
   if (kseg > 0) issue(r0, 0);
+#if FEDAVG_NNADQ_ASM
+  // group i's loads retire with vmcnt(G) when group i + 1's G loads were issued after them,
+  // vmcnt(0) otherwise
+  auto retire = [&](bool next_issued) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (next_issued) {
+      __builtin_amdgcn_s_waitcnt((G & 15) | ((G >> 4) << 14) | (7 << 4) | (15 << 8));
+    } else {
+      __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int k = 0; k < kseg; k += 2 * G) {
+    const bool second = k + G < kseg;
+    if (second) issue(r1, k + G);
+    retire(second);
+    run(r0, k);
+    if (second) {
+      const bool third = k + 2 * G < kseg;
+      if (third) issue(r0, k + 2 * G);
+      retire(third);
+      run(r1, k + G);
+    }
+  }
+#else
   for (int k = 0; k < kseg; k += 2 * G) {
     const bool second = k + G < kseg;
     if (second) issue(r1, k + G);
@@ -1335,6 +1423,7 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
       run(r1, k + G);
     }
   }
+#endif
   have = have || (kseg > 0);
   if (!have) return;
   record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);

@@ -1,6 +1,7 @@
 """HBM traffic of a bench line's FedAvg kernels from a scripts/gpu_config_traffic.sh pass set.
 
-Usage: python scripts/traffic_summary.py OUT_DIR NAME TAG
+Usage: python scripts/traffic_summary.py OUT_DIR NAME TAG [KERNEL]   (KERNEL: fedavg_tile_kernel by
+default; qsgd_tile_kernel / nnadq_tile_kernel for the quantised lines)
   OUT_DIR/NAME_trace  rocprofv3 --kernel-trace --stats   (+ the bench JSON line in NAME_trace.log)
   OUT_DIR/NAME_fetch  rocprofv3 --pmc FETCH_SIZE          (separate passes: TCC slot limits)
   OUT_DIR/NAME_write  rocprofv3 --pmc WRITE_SIZE
@@ -21,7 +22,7 @@ out_dir, name, tag = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
 repo = Path(__file__).resolve().parent.parent
 prof = repo / "profiles"
 PROBE_BYTES = 4 << 30
-KERNEL = "fedavg_tile_kernel"
+KERNEL = sys.argv[4] if len(sys.argv) > 4 else "fedavg_tile_kernel"
 
 
 def counter(pass_dir, kernel_substr):
@@ -39,14 +40,15 @@ write = statistics.mean(counter(f"{name}_write", KERNEL)) * 1024 * write_corr
 r = line["roofline"]
 per_step_launches = r["launches"] / line["steps"]
 traffic_step = (fetch + write) * per_step_launches
-alg_step = r.get("bytes_per_step_this_rank") or r.get("bytes_per_timed_launch")
+alg_step = (r.get("bytes_per_step_this_rank") or r.get("bytes_per_timed_launch")
+            or (r.get("bytes_per_launch", 0) * per_step_launches or None))
 out = {
     "tag": tag,
     "workload": line["config"]["workload"],
     "kernel": KERNEL,
     "launches_per_step": per_step_launches,
     "kernel_avg_ms_rocprof": None if avg_ns is None else avg_ns / 1e6,
-    "kernel_ms_per_step_hip_events": r["kernel_ms_per_step"],
+    "kernel_ms_per_step_hip_events": r.get("kernel_ms_per_step", r.get("mean_launch_ms")),
     "fetch_bytes_per_launch": fetch,
     "write_bytes_per_launch": write,
     "hbm_traffic_bytes_per_step": traffic_step,

@@ -870,7 +870,13 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
 #endif
 static_assert(FEDAVG_QSGD_AE == 16 || FEDAVG_QSGD_AE == 8, "QSGD lanes hold 16 or 8 elements");
 // one wave of the workgroup DMAs each client table of a group: clients per group = waves
-#define FEDAVG_QSGD_GROUP (4096 / FEDAVG_QSGD_AE / 64)
+#ifndef FEDAVG_QSGD_GROUP  // clients per group, at most one per wave (2: 82 VGPRs, 5 waves/SIMD)
+#define FEDAVG_QSGD_GROUP 2
+#endif
+#ifndef FEDAVG_QSGD_RB  // table reads per batch before their adds (elements of a lane)
+#define FEDAVG_QSGD_RB 4
+#endif
+static_assert(FEDAVG_QSGD_GROUP >= 1 && FEDAVG_QSGD_GROUP <= 4096 / FEDAVG_QSGD_AE / 64, "one table DMA per wave");
 constexpr int kQsgdGroup = FEDAVG_QSGD_GROUP;
 #ifndef FEDAVG_QSGD_DEPTH
 #define FEDAVG_QSGD_DEPTH 1
@@ -1088,8 +1094,11 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
         asm volatile("global_load_ubyte %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
       }
     }
-    const double* src = tabs + static_cast<int64_t>(k + min(wave, n - 1)) * kQsgdTable;
-    double* dst = lut[buf][wave];
+    // waves past the group's size move the group's last table again, into its own slot (the
+    // same bytes twice: every wave issues the same DMAs, so the counted wait holds)
+    const int tw = min(wave, G - 1);
+    const double* src = tabs + static_cast<int64_t>(k + min(tw, n - 1)) * kQsgdTable;
+    double* dst = lut[buf][tw];
     __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 128 + 2 * lane),
@@ -1146,32 +1155,38 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
         const int32_t t0hi = reinterpret_cast<const int32_t*>(tab)[1];  // broadcast read
         // per element: 1 = negative product
         const uint32_t neg = r.signs[c] ^ ~static_cast<uint32_t>(t0hi >> 31);
-        // all 16 table reads of this client in flight before the first add (the compiler
-        // otherwise keeps ~4 outstanding and waits on each batch)
-        double pav[AE];
+        // RB table reads in flight before their adds (all 16 by default; the compiler would
+        // otherwise keep ~4 outstanding and wait on each batch); fewer per batch = fewer VGPRs
+        constexpr int RB = FEDAVG_QSGD_RB < AE ? FEDAVG_QSGD_RB : AE;
 #pragma unroll
-        for (int j = 0; j < AE; ++j) {
-          const uint32_t word = r.slots[c][j >> 2];
-          const uint32_t off = ((word >> (8 * (j & 3))) & 0xffu) << 3;
+        for (int j0 = 0; j0 < AE; j0 += RB) {
+          double pav[RB];
+#pragma unroll
+          for (int jj = 0; jj < RB; ++jj) {
+            const int j = j0 + jj;
+            const uint32_t word = r.slots[c][j >> 2];
+            const uint32_t off = ((word >> (8 * (j & 3))) & 0xffu) << 3;
 #if FEDAVG_QSGD_ABLATE == 1  // timing only: no table reads (wrong results)
-          pav[j] = static_cast<double>(off);
+            pav[jj] = static_cast<double>(off);
 #else
-          pav[j] = *reinterpret_cast<const double*>(tab + off);
+            pav[jj] = *reinterpret_cast<const double*>(tab + off);
 #endif
-        }
+          }
 #if FEDAVG_QSGD_READ_FENCE
-        __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
 #endif
 #pragma unroll
-        for (int j = 0; j < AE; ++j) {
-          // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte of
-          // the little-endian sign word, element j >= 8 bit 15 - (j - 8)
-          const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
-          const uint32_t sb = neg << (31 - bit);
-          const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pav[j]));
-          const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
-          const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
-          acc[j] = acc[j] + p;
+          for (int jj = 0; jj < RB; ++jj) {
+            const int j = j0 + jj;
+            // numpy.packbits order: element j < 8 of this lane is bit 7 - j of the low byte of
+            // the little-endian sign word, element j >= 8 bit 15 - (j - 8)
+            const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
+            const uint32_t sb = neg << (31 - bit);
+            const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pav[jj]));
+            const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
+            const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
+            acc[j] = acc[j] + p;
+          }
         }
       }
     }

@@ -152,7 +152,10 @@ def test_fedavg_balanced_head_bit_identical(hip_device, d, monkeypatch):
 
 @pytest.mark.parametrize("i", range(6))
 def test_qsgd_kernel_edges_bit_identical(hip_device, i):
-    n = around(K("qsgd_group"), 2 * K("qsgd_group"))[i]  # (the library is read at run time, not collection)
+    counts = around(K("qsgd_group"), 2 * K("qsgd_group"))  # (the library is read at run time, not collection)
+    if i >= len(counts):
+        pytest.skip(f"{len(counts)} client counts around the library's group size")
+    n = counts[i]
     lengths = around(K("qsgd_ae"), K("qsgd_tile"), 2 * K("qsgd_tile"))
     rng = np.random.default_rng(n)
     recs = [[qo.quantize(rng.standard_normal(m).astype(np.float32), rng) for m in lengths] for _ in range(n)]

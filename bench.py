@@ -713,8 +713,8 @@ def main_plugin(args: argparse.Namespace) -> int:
     buckets, views = make_clients(layout, 0, N, device, in_dtype)
     params = [{n: v.view(s) for n, s, v in zip(layout.names, layout.shapes, row)} for row in views]
     weights = dataset_size_weights(N)
-    wave = args.wave if args.wave > 0 else N
-    algo = FedAVGAlgorithm(device=device, wave_size=wave, result_dtype=out_dtype)
+    algo = FedAVGAlgorithm(device=device, wave_size=args.wave if args.wave > 0 else None, result_dtype=out_dtype)
+    wave = min(algo.wave_size, N)  # the plugin's own default unless --wave is given
 
     # --workload gradient: GradientWorker._process_gradient's message every step (gradient_worker.py:
     # 83-93): the native-dtype gradient dict, in_round=True, the dataset size as weight

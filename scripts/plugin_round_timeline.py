@@ -1,0 +1,112 @@
+"""Where a plugin round's time goes beyond its kernel (GPU box): 64 device-resident ResNet-18 fp32
+updates through FedAVGAlgorithm (one wave), wall-clock marks around the pieces of
+aggregate_worker_data (FedAvgContext.aggregate = staging + enqueue, raise_on_nan = the sync + NaN
+flags, the rest = result views / message), with the kernel's own duration from the library's
+profiling events. Prints one JSON line (means over R rounds, microseconds)."""
+from __future__ import annotations
+
+import json
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+import torch  # noqa: E402
+
+from bench import dataset_size_weights, make_clients, resnet18_layout  # noqa: E402
+from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMessage  # noqa: E402
+from distributed_learning_simulation_lib_amd.fedavg import FedAvgContext  # noqa: E402
+
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+R = 40
+dev = torch.device("cuda", 0)
+layout = resnet18_layout()
+w = dataset_size_weights(K)
+_, views = make_clients(layout, 0, K, dev, torch.float32)
+params = [{n: v.view(s) for n, s, v in zip(layout.names, layout.shapes, row)} for row in views]
+
+marks: dict[str, float] = {}
+_agg, _nan = FedAvgContext.aggregate, FedAvgContext.raise_on_nan
+
+
+def agg(self, *a, **k):
+    marks["agg_in"] = time.perf_counter()
+    r = _agg(self, *a, **k)
+    marks["agg_out"] = time.perf_counter()
+    return r
+
+
+def nan(self, *a, **k):
+    marks["nan_in"] = time.perf_counter()
+    r = _nan(self, *a, **k)
+    marks["nan_out"] = time.perf_counter()
+    return r
+
+
+_reset = FedAvgContext.reset
+reset_acc = [0.0, 0]
+
+
+def reset(self, *a, **k):
+    t = time.perf_counter()
+    r = _reset(self, *a, **k)
+    reset_acc[0] += time.perf_counter() - t
+    reset_acc[1] += 1
+    return r
+
+
+FedAvgContext.aggregate, FedAvgContext.raise_on_nan, FedAvgContext.reset = agg, nan, reset
+algo = FedAVGAlgorithm(device=dev, wave_size=K)
+msgs = lambda: [ParameterMessage(parameter=dict(p), aggregation_weight=x) for p, x in zip(params, w)]  # noqa: E731
+for _ in range(3):
+    for i, m in enumerate(msgs()):
+        algo.process_worker_data(i, m)
+    algo.aggregate_worker_data()
+    algo.clear_worker_data()
+torch.cuda.synchronize()
+ctx = algo._context()
+ctx.prof_collect()
+ctx.prof_enable(True)
+acc = {k: 0.0 for k in ("process", "to_agg", "aggregate_call", "between", "sync_and_flags", "after", "clear", "round")}
+for _ in range(R):
+    ms = msgs()
+    t0 = time.perf_counter()
+    for i, m in enumerate(ms):
+        algo.process_worker_data(i, m)
+    t1 = time.perf_counter()
+    algo.aggregate_worker_data()
+    t2 = time.perf_counter()
+    algo.clear_worker_data()
+    t3 = time.perf_counter()
+    acc["process"] += t1 - t0
+    acc["to_agg"] += marks["agg_in"] - t1
+    acc["aggregate_call"] += marks["agg_out"] - marks["agg_in"]
+    acc["between"] += marks["nan_in"] - marks["agg_out"]
+    acc["sync_and_flags"] += marks["nan_out"] - marks["nan_in"]
+    acc["after"] += t2 - marks["nan_out"]
+    acc["clear"] += t3 - t2
+    acc["round"] += t3 - t0
+torch.cuda.synchronize()
+kernel_ms, launches = ctx.prof_collect()
+# split of "after": the pieces aggregate_worker_data runs once the flags are read
+import cProfile, pstats, io  # noqa: E402,E401
+ms = msgs()
+for i, m in enumerate(ms):
+    algo.process_worker_data(i, m)
+pr = cProfile.Profile()
+pr.enable()
+algo.aggregate_worker_data()
+pr.disable()
+algo.clear_worker_data()
+buf = io.StringIO()
+pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(12)
+print(buf.getvalue(), file=sys.stderr)
+out = {k + "_us": round(v / R * 1e6, 1) for k, v in acc.items()}
+out["kernel_us"] = round(kernel_ms * 1e3 / max(launches, 1), 1)
+out["launches_per_round"] = launches / R
+out["clients"] = K
+out["reset_us_per_call"] = round(reset_acc[0] / max(reset_acc[1], 1) * 1e6, 1)
+out["reset_calls_per_round"] = reset_acc[1] / (R + 3)
+print(json.dumps(out))

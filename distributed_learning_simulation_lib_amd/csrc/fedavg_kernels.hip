@@ -886,9 +886,21 @@ constexpr int kQsgdDepth = FEDAVG_QSGD_DEPTH;
 constexpr int kQsgdBufs = kQsgdDepth + 1;
 static_assert(kQsgdDepth >= 1 && kQsgdDepth <= 3, "QSGD prefetch depth 1..3");
 
-constexpr int kQsgdTable = 256;  // entries per client (|p| per slot value)
+#ifndef FEDAVG_QSGD_SIGNED  // 1: 512-entry signed tables indexed by (non-negative << 8 | slot)
+#define FEDAVG_QSGD_SIGNED 0
+#endif
+constexpr int kQsgdSlots = 256;  // slot values
+// table entries per client: |p| per slot value, or (signed form) -p | +p per slot value
+constexpr int kQsgdTable = FEDAVG_QSGD_SIGNED ? 512 : 256;
+#ifndef FEDAVG_QSGD_DMA_SPLIT  // 1: a group's table chunks split over the waves (no duplicate DMAs)
+#define FEDAVG_QSGD_DMA_SPLIT 1
+#endif
+#ifndef FEDAVG_QSGD_SOLO  // 1: one-wave workgroups (a quarter tile each) that DMA their own tables
+#define FEDAVG_QSGD_SOLO 0
+#endif
 constexpr int kQsgdAE = FEDAVG_QSGD_AE;
-constexpr int kQsgdLanes = 4096 / kQsgdAE;
+constexpr int kQsgdTileLanes = 4096 / kQsgdAE;  // lanes covering one 4096-element tile
+constexpr int kQsgdLanes = FEDAVG_QSGD_SOLO ? 64 : kQsgdTileLanes;  // lanes per workgroup
 
 template <typename DQ>
 __device__ __forceinline__ double qsgd_product(double norm, int level, int slot, double w) {
@@ -907,7 +919,7 @@ __device__ __forceinline__ double qsgd_product(double norm, int level, int slot,
 // of the segments [seg_begin, seg_begin + gridDim.y); 2 KiB per table, L2 / MALL resident for
 // the tile kernel's LDS-DMA loads.
 template <typename DQ>
-__global__ __launch_bounds__(kQsgdTable) void qsgd_table_kernel(CallTables tab, int32_t K, int32_t seg_begin,
+__global__ __launch_bounds__(kQsgdSlots) void qsgd_table_kernel(CallTables tab, int32_t K, int32_t seg_begin,
                                                                 double* qtab) {
   const int seg = seg_begin + static_cast<int>(blockIdx.y);
   const int k = static_cast<int>(blockIdx.x);
@@ -918,6 +930,15 @@ __global__ __launch_bounds__(kQsgdTable) void qsgd_table_kernel(CallTables tab, 
   const int level = to_const<int32_t>(rec)[2];
   const double w = to_const<double>(tab.w)[row];
   const int s = static_cast<int>(threadIdx.x);
+#if FEDAVG_QSGD_SIGNED
+  // entry 256 + s: the product of a non-negative element of slot s (sign(norm) * sign(w)),
+  // entry s: its negation, the product of a negative element (every step is sign-symmetric,
+  // zeros included), so the fold indexes the table with (sign bit << 8 | slot) and adds
+  const double pp = qsgd_product<DQ>(norm, level, s, w);
+  qtab[row * kQsgdTable + kQsgdSlots + s] = pp;
+  qtab[row * kQsgdTable + s] = -pp;
+  return;
+#endif
   const double p = __builtin_fabs(qsgd_product<DQ>(norm, level, s, w));
   // entry 0 is a zero (or a NaN, for a non-finite norm / weight): its sign bit carries the
   // client's product sign, signbit(norm) ^ signbit(w), which the fold reads with one broadcast
@@ -1038,14 +1059,15 @@ __device__ __forceinline__ void qsgd_wait_vmcnt() {
 }
 
 template <int OUT, typename DQ, bool FULL, bool VEC>
-__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable]) {
+__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable],
+                                               int lane_base) {
   constexpr int AE = kQsgdAE;
   constexpr int G = kQsgdGroup;
   constexpr int D = kQsgdDepth;
   constexpr int NB = kQsgdBufs;
   const int seg = td.seg;
   const int count = td.count;
-  const int li = static_cast<int>(threadIdx.x);
+  const int li = lane_base + static_cast<int>(threadIdx.x);
   const int e0 = li * AE;  // first element of this lane within the tile
   const bool lane_live = FULL || e0 < count;
 
@@ -1067,7 +1089,17 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   // last client again for a short group), issued D groups ahead of the group's fold into one of
   // D + 1 LDS buffers: every wave issues exactly kOps vector memory operations per group, so
   // "the group D - 1 issues back has landed" is a counted vmcnt.
-  constexpr int kOps = 2 * G + 2;
+  // DMA chunks of 1 KiB per wave and group: a 2-KiB table per client over the group's waves
+  // (waves past the group's size repeat the last table), or the 4-KiB signed tables spread
+  // evenly over the waves
+  constexpr int kWaves = kQsgdLanes / 64;
+  constexpr int kChunks = G * kQsgdTable / 128;  // 1-KiB DMA chunks of a group's tables
+  // the chunks split evenly over the waves (no wave moves a table twice), or — when they do not
+  // — wave w moves client min(w, G - 1)'s whole table (waves past the group repeat the last one)
+  constexpr bool kSplit = FEDAVG_QSGD_SOLO || (FEDAVG_QSGD_DMA_SPLIT && kChunks % kWaves == 0);
+  constexpr int kDmaPerWave = kSplit ? kChunks / kWaves : 2;
+  static_assert(!FEDAVG_QSGD_SIGNED || kSplit, "signed tables split evenly over the waves");
+  constexpr int kOps = 2 * G + kDmaPerWave;
   using SlotVec = typename std::conditional<AE == 16, u32x4, u32x2>::type;  // AE slot bytes
   struct GroupRegs {
     SlotVec slots[G];
@@ -1094,6 +1126,19 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
         asm volatile("global_load_ubyte %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
       }
     }
+    if constexpr (kSplit) {
+#pragma unroll
+    for (int q = 0; q < kDmaPerWave; ++q) {
+      // 1-KiB chunk of the group's tables (a one-wave workgroup moves all of them)
+      const int chunk = (FEDAVG_QSGD_SOLO ? 0 : wave * kDmaPerWave) + q;
+      const int cl = chunk / (kQsgdTable / 128);    // client of the group
+      const int part = chunk % (kQsgdTable / 128);  // 128 doubles each
+      const double* src = tabs + static_cast<int64_t>(k + min(cl, n - 1)) * kQsgdTable + part * 128;
+      double* dst = lut[buf][cl] + part * 128;
+      __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
+                                       (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+    }
+    } else {
     // waves past the group's size move the group's last table again, into its own slot (the
     // same bytes twice: every wave issues the same DMAs, so the counted wait holds)
     const int tw = min(wave, G - 1);
@@ -1103,6 +1148,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 128 + 2 * lane),
                                      (void __attribute__((address_space(3)))*)(dst + 128), 16, 0, 0);
+    }
   };
   // Fold of one group from LDS buffer B (compile-time, so every table read is
   // `ds_read_b64 v, v_off offset:<buffer base>`). The table holds |p|; the sign of each
@@ -1143,6 +1189,44 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
           const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
           const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
           acc[j] = acc[j] + p;
+        }
+      }
+    }
+    return;
+#endif
+#if FEDAVG_QSGD_SIGNED
+    static_assert(AE == 16, "the signed fold spreads a 16-bit sign word");
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c < n) {
+        const char* tab = reinterpret_cast<const char*>(lut[B][c]);
+        // numpy.packbits order puts element j < 8 at bit 7 - j and j >= 8 at bit 23 - j of the
+        // 16-bit word (1 = non-negative); reversed, element j sits at bit 24 + j (j < 8) or
+        // 8 + j (j >= 8): four consecutive elements are one nibble
+        const uint32_t rev = __builtin_bitreverse32(r.signs[c]);
+#pragma unroll
+        for (int q = 0; q < AE / 4; ++q) {  // elements 4q .. 4q + 3: slot word q
+          const int pos = (q < 2) ? 24 + 4 * q : 8 + 4 * q;
+          // nibble -> one byte per element (bit i -> bit 8 i), each 0 or 1
+          const uint32_t sb4 = (((rev >> pos) & 0xfu) * 0x00204081u) & 0x01010101u;
+          const uint32_t word = r.slots[c][q];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // elements 4q + 2h, 4q + 2h + 1
+            // two 16-bit table indices (sign << 8 | slot) in one v_perm_b32
+            const uint32_t sel = h ? 0x07030602u : 0x05010400u;
+            const uint32_t idx2 = __builtin_amdgcn_perm(sb4, word, sel);
+            // byte offsets: the low index by one SDWA shift of its word (the compiler emits a
+            // shift + mask), the high one as idx2 >> 13 (bits 13-15 of the low index are 0)
+            uint32_t off0;
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                : "=v"(off0) : "v"(3u), "v"(idx2));
+            const uint32_t off1 = idx2 >> 13;
+            double pv[2];
+            pv[0] = *reinterpret_cast<const double*>(tab + off0);
+            pv[1] = *reinterpret_cast<const double*>(tab + off1);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) acc[4 * q + 2 * h + e] = acc[4 * q + 2 * h + e] + pv[e];
+          }
         }
       }
     }
@@ -1229,11 +1313,15 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
 template <int OUT, typename DQ, bool VEC>
 __global__ __launch_bounds__(kQsgdLanes) void qsgd_tile_kernel(KArgs a) {
   __shared__ double lut[kQsgdBufs][kQsgdGroup][kQsgdTable];
-  const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
+  constexpr int kParts = kQsgdTileLanes / kQsgdLanes;  // workgroups per tile
+  const int bid = static_cast<int>(blockIdx.x);
+  const TileDesc td = load_tile(a.tiles, a.tile_begin + bid / kParts);
+  const int lane_base = (bid % kParts) * kQsgdLanes;
+  if (kParts > 1 && lane_base * kQsgdAE >= td.count) return;  // a quarter past a short tile's end
   if (td.count == kTile1) {
-    qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut);
+    qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut, lane_base);
   } else {
-    qsgd_tile_body<OUT, DQ, false, VEC>(a, td, lut);
+    qsgd_tile_body<OUT, DQ, false, VEC>(a, td, lut, lane_base);
   }
 }
 
@@ -2141,12 +2229,12 @@ hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream
   // the call's |product| tables first (same stream: the tile kernel reads them by DMA)
   const dim3 tgrid(static_cast<unsigned>(a.K), static_cast<unsigned>(seg_count));
   if (in_dtype == FEDAVG_QSGD_F32)
-    hipLaunchKernelGGL(qsgd_table_kernel<float>, tgrid, dim3(kQsgdTable), 0, s, a.tab, a.K, seg_begin,
+    hipLaunchKernelGGL(qsgd_table_kernel<float>, tgrid, dim3(kQsgdSlots), 0, s, a.tab, a.K, seg_begin,
                        const_cast<double*>(a.qtab));
   else
-    hipLaunchKernelGGL(qsgd_table_kernel<double>, tgrid, dim3(kQsgdTable), 0, s, a.tab, a.K, seg_begin,
+    hipLaunchKernelGGL(qsgd_table_kernel<double>, tgrid, dim3(kQsgdSlots), 0, s, a.tab, a.K, seg_begin,
                        const_cast<double*>(a.qtab));
-  const dim3 grid(static_cast<unsigned>(a.num_tiles)), block(kQsgdLanes);
+  const dim3 grid(static_cast<unsigned>(a.num_tiles * (kQsgdTileLanes / kQsgdLanes))), block(kQsgdLanes);
   if (in_dtype == FEDAVG_QSGD_F32) {
     if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true>), grid, block, 0, s, nullptr, e1, 0, a);
     else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, false>), grid, block, 0, s, nullptr, e1, 0, a);

@@ -892,6 +892,12 @@ static_assert(kQsgdDepth >= 1 && kQsgdDepth <= 3, "QSGD prefetch depth 1..3");
 constexpr int kQsgdSlots = 256;  // slot values
 // table entries per client: |p| per slot value, or (signed form) -p | +p per slot value
 constexpr int kQsgdTable = FEDAVG_QSGD_SIGNED ? 512 : 256;
+#ifndef FEDAVG_QSGD_WPE  // > 0: ask the compiler for at least this many waves per SIMD
+#define FEDAVG_QSGD_WPE 0
+#endif
+#ifndef FEDAVG_QSGD_WIDE  // 1: whole-layout launches fold 8192-element tiles (512 lanes)
+#define FEDAVG_QSGD_WIDE 0
+#endif
 #ifndef FEDAVG_QSGD_DMA_SPLIT  // 1: a group's table chunks split over the waves (no duplicate DMAs)
 #define FEDAVG_QSGD_DMA_SPLIT 1
 #endif
@@ -1058,7 +1064,7 @@ __device__ __forceinline__ void qsgd_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int OUT, typename DQ, bool FULL, bool VEC>
+template <int OUT, typename DQ, bool FULL, bool VEC, int TILEN = 4096>
 __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable],
                                                int lane_base) {
   constexpr int AE = kQsgdAE;
@@ -1092,12 +1098,16 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   // DMA chunks of 1 KiB per wave and group: a 2-KiB table per client over the group's waves
   // (waves past the group's size repeat the last table), or the 4-KiB signed tables spread
   // evenly over the waves
-  constexpr int kWaves = kQsgdLanes / 64;
+  constexpr int kWaves = (FEDAVG_QSGD_SOLO ? kQsgdLanes : TILEN / AE) / 64;
   constexpr int kChunks = G * kQsgdTable / 128;  // 1-KiB DMA chunks of a group's tables
+  // more waves than chunks (8192-element tiles): waves past the chunks move nothing — their
+  // operation count differs, which only the one-group-ahead schedule (vmcnt(0) waits) allows
+  constexpr bool kSparse = !FEDAVG_QSGD_SOLO && kChunks < kWaves && FEDAVG_QSGD_DMA_SPLIT;
+  static_assert(!kSparse || kQsgdDepth == 1, "uneven DMA counts need the vmcnt(0) schedule");
   // the chunks split evenly over the waves (no wave moves a table twice), or — when they do not
   // — wave w moves client min(w, G - 1)'s whole table (waves past the group repeat the last one)
   constexpr bool kSplit = FEDAVG_QSGD_SOLO || (FEDAVG_QSGD_DMA_SPLIT && kChunks % kWaves == 0);
-  constexpr int kDmaPerWave = kSplit ? kChunks / kWaves : 2;
+  constexpr int kDmaPerWave = kSplit ? kChunks / kWaves : kSparse ? 1 : 2;
   static_assert(!FEDAVG_QSGD_SIGNED || kSplit, "signed tables split evenly over the waves");
   constexpr int kOps = 2 * G + kDmaPerWave;
   using SlotVec = typename std::conditional<AE == 16, u32x4, u32x2>::type;  // AE slot bytes
@@ -1126,7 +1136,16 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
         asm volatile("global_load_ubyte %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
       }
     }
-    if constexpr (kSplit) {
+    if constexpr (kSparse) {
+      if (wave < kChunks) {  // wave-uniform
+        const int cl = wave / (kQsgdTable / 128);
+        const int part = wave % (kQsgdTable / 128);
+        const double* src = tabs + static_cast<int64_t>(k + min(cl, n - 1)) * kQsgdTable + part * 128;
+        double* dst = lut[buf][cl] + part * 128;
+        __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
+                                         (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+      }
+    } else if constexpr (kSplit) {
 #pragma unroll
     for (int q = 0; q < kDmaPerWave; ++q) {
       // 1-KiB chunk of the group's tables (a one-wave workgroup moves all of them)
@@ -1310,18 +1329,24 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
 }
 
-template <int OUT, typename DQ, bool VEC>
-__global__ __launch_bounds__(kQsgdLanes) void qsgd_tile_kernel(KArgs a) {
+// TILEN = 4096 (kTile1 table: every launch) or 8192 (kTileWide table, 512 lanes: whole-layout
+// launches — half the table traffic per element)
+template <int OUT, typename DQ, bool VEC, int TILEN = 4096>
+__global__ __launch_bounds__(TILEN == 4096 ? kQsgdLanes : TILEN / kQsgdAE)
+#if FEDAVG_QSGD_WPE
+__attribute__((amdgpu_waves_per_eu(FEDAVG_QSGD_WPE)))
+#endif
+void qsgd_tile_kernel(KArgs a) {
   __shared__ double lut[kQsgdBufs][kQsgdGroup][kQsgdTable];
-  constexpr int kParts = kQsgdTileLanes / kQsgdLanes;  // workgroups per tile
+  constexpr int kParts = TILEN == 4096 ? kQsgdTileLanes / kQsgdLanes : 1;  // workgroups per tile
   const int bid = static_cast<int>(blockIdx.x);
   const TileDesc td = load_tile(a.tiles, a.tile_begin + bid / kParts);
   const int lane_base = (bid % kParts) * kQsgdLanes;
   if (kParts > 1 && lane_base * kQsgdAE >= td.count) return;  // a quarter past a short tile's end
-  if (td.count == kTile1) {
-    qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut, lane_base);
+  if (td.count == TILEN) {
+    qsgd_tile_body<OUT, DQ, true, VEC, TILEN>(a, td, lut, lane_base);
   } else {
-    qsgd_tile_body<OUT, DQ, false, VEC>(a, td, lut, lane_base);
+    qsgd_tile_body<OUT, DQ, false, VEC, TILEN>(a, td, lut, lane_base);
   }
 }
 
@@ -2225,7 +2250,7 @@ hipError_t launch_nnadq_out(int32_t in_dtype, const KArgs& a, bool vec, bool fma
 
 template <int OUT>
 hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1, int32_t seg_begin,
-                           int32_t seg_count) {
+                           int32_t seg_count, bool wide = false) {
   // the call's |product| tables first (same stream: the tile kernel reads them by DMA)
   const dim3 tgrid(static_cast<unsigned>(a.K), static_cast<unsigned>(seg_count));
   if (in_dtype == FEDAVG_QSGD_F32)
@@ -2234,6 +2259,19 @@ hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream
   else
     hipLaunchKernelGGL(qsgd_table_kernel<double>, tgrid, dim3(kQsgdSlots), 0, s, a.tab, a.K, seg_begin,
                        const_cast<double*>(a.qtab));
+  if constexpr (FEDAVG_QSGD_WIDE && kTileWide == 8192 && !FEDAVG_QSGD_SOLO) {
+    if (wide) {  // a.tiles is the kTileWide table
+      const dim3 gw(static_cast<unsigned>(a.num_tiles)), bw(8192 / kQsgdAE);
+      if (in_dtype == FEDAVG_QSGD_F32) {
+        if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
+        else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, false, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
+      } else {
+        if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, double, true, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
+        else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, double, false, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
+      }
+      return hipGetLastError();
+    }
+  }
   const dim3 grid(static_cast<unsigned>(a.num_tiles * (kQsgdTileLanes / kQsgdLanes))), block(kQsgdLanes);
   if (in_dtype == FEDAVG_QSGD_F32) {
     if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true>), grid, block, 0, s, nullptr, e1, 0, a);
@@ -2371,10 +2409,18 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     a.qtab = c->qtab;
     const int32_t seg0 = c->tiles1[tb_split1].seg;
     const int32_t nseg = c->tiles1[te_split1 - 1].seg - seg0 + 1;
+    // a whole-layout launch folds the 8192-element tiles (half the table traffic per element)
+    const bool qwide = FEDAVG_QSGD_WIDE && c->d_tilesw != nullptr && tb_split1 == 0 &&
+                       te_split1 == static_cast<int32_t>(c->tiles1.size());
+    if (qwide) {
+      a.tiles = c->d_tilesw;
+      a.tile_begin = 0;
+      a.num_tiles = static_cast<int>(c->tilesw.size());
+    }
     switch (out_kind) {
-      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
-      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
-      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
+      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1, seg0, nseg, qwide); break;
+      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1, seg0, nseg, qwide); break;
+      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1, seg0, nseg, qwide); break;
       default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
     }
     if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));

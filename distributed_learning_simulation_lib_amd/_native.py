@@ -30,6 +30,8 @@ ERR_STATE = 6
 ERR_RCCL = 7
 COMM_ID_BYTES = 128
 EXCHANGE_REDUCE, EXCHANGE_SCATTER = 0, 1  # FEDAVG_EXCHANGE_* (fedavg_sharded_round_edges)
+EXCHANGE_PEER = 2  # fedavg_multi_round / _combine: peer-window stores, no collective library
+MULTI_MAX_DEVICES = 16
 FLAG_ACC_NAN = 0x1
 FLAG_RESULT_NAN = 0x2
 FLAG_CENTRAL_NAN = 0x4
@@ -104,6 +106,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_plan_run_range": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_plan_destroy": (c_int32, [c_void_p]),
     "fedavg_set_segment_state": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
+    "fedavg_segment_state": (c_int32, [c_void_p, _PD, POINTER(c_int32)]),
     "fedavg_accumulate_elementwise": (
         c_int32, [c_void_p, _PP, c_int32, _PP, POINTER(c_int32), _PD, POINTER(c_int32), c_int32, c_void_p, c_void_p]),
     "fedavg_finalize_elementwise": (c_int32, [c_void_p, c_void_p, _PP, c_int32, c_void_p]),
@@ -142,6 +145,19 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_sharded_round_edges": (
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int32), c_int32, c_int32, c_int32, c_void_p]),
+    # single-process multi-device mode (multi_device.cpp)
+    "fedavg_multi_create": (c_int32, [POINTER(c_void_p), POINTER(c_int32), c_int32, POINTER(c_int64), c_int32, _PP]),
+    "fedavg_multi_destroy": (c_int32, [c_void_p]),
+    "fedavg_multi_num_devices": (c_int32, [c_void_p]),
+    "fedavg_multi_device": (c_int32, [c_void_p, c_int32]),
+    "fedavg_multi_context": (c_void_p, [c_void_p, c_int32]),
+    "fedavg_multi_stream": (c_void_p, [c_void_p, c_int32]),
+    "fedavg_multi_peer_access": (c_int32, [c_void_p]),
+    "fedavg_multi_round": (
+        c_int32, [c_void_p, _PP, _PD, _PP, c_int32, c_int32, POINTER(c_int32), c_int32, c_int32, _PP]),
+    "fedavg_multi_combine": (c_int32, [c_void_p, _PD, _PP, c_int32, c_int32, c_int32, _PP]),
+    "fedavg_multi_check": (c_int32, [c_void_p, POINTER(c_uint32)]),
+    "fedavg_multi_reset": (c_int32, [c_void_p]),
 }
 
 _lib: ctypes.CDLL | None = None

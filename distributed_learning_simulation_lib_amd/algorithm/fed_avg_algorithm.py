@@ -36,16 +36,17 @@ Differences a caller can observe, all documented in DESIGN.md:
 from __future__ import annotations
 
 import os
-from collections.abc import MutableMapping
+from collections.abc import MutableMapping, Sequence
 from typing import Any
 
 import numpy as np
 import torch
 
-from .. import _staging
+from .. import _native, _staging
 from .._staging import NativeClientTable
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
+from ..multi_device import MultiDeviceContext
 from ..message import (
     KIND_DELTA,
     KIND_PARAMETER,
@@ -71,6 +72,11 @@ _STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64) 
 _STAGING_CODES = {dt: code for code, dt in enumerate(_STAGING_DTYPES)}
 # host QSGD records packed by pointer (FEDAVG_QSGD_HOST_PTRS=0: through per-record views, A/B knob)
 _HOST_RECORD_PTRS = os.environ.get("FEDAVG_QSGD_HOST_PTRS", "1") != "0"
+# what a device entry of the multi-device mode keeps for itself (the rest of the round's state —
+# layout, per-name totals, flags — is one for the whole round)
+_LANE_ATTRS = ("_device", "_FedAVGAlgorithm__table", "_FedAVGAlgorithm__table_dtype",
+               "_FedAVGAlgorithm__table_delta", "_FedAVGAlgorithm__ingest", "_FedAVGAlgorithm__fast",
+               "_FedAVGAlgorithm__base")
 
 
 def _is_elementwise(weight: Any, parameter: Any) -> bool:
@@ -108,6 +114,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         result_device: torch.device | str | None = None,
         split_policy: int = 1,
         eager_nan_check: bool | None = None,
+        devices: Sequence[int | str | torch.device] | None = None,
+        exchange: str = "peer",
     ) -> None:
         super().__init__()
         self.accumulate: bool = True
@@ -158,6 +166,28 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                                    for h in ("_accumulate_parameter", "_get_weight", "_note_total"))
         self.__tot_fp32: dict[str, bool] = {}
         self.__ew_totals: torch.Tensor | None = None
+        # Multi-device mode (one server process, several MI355X; include/fedavg_hip.h fedavg_multi_*):
+        # arrivals are dealt to the device entries in turn (an update already resident on a GPU goes
+        # to an entry of that GPU), each entry folds its shard in waves like the single-device path,
+        # and aggregate_worker_data sums the G partials in entry order on the GPUs (``exchange``:
+        # "peer" stores over xGMI, or "reduce": RCCL) and divides into the first entry's device.
+        self.__multi_devices: list[torch.device] | None = None
+        self.__multi: MultiDeviceContext | None = None
+        self.__lanes: list[dict[str, Any]] = []
+        self.__lane = 0
+        self.__arrivals = 0
+        self.exchange = exchange
+        if devices is not None:
+            devs = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in devices]
+            if not devs or any(d.type != "cuda" for d in devs):
+                raise ValueError("devices: a non-empty list of GPU devices")
+            if device is not None and torch.device(device) != devs[0]:
+                raise ValueError("device must be the first entry of devices (the result's device)")
+            self._device = devs[0]
+            self.__multi_devices = devs
+            self.__lanes = [{a: getattr(self, a) for a in _LANE_ATTRS} for _ in devs]
+            for lane, d in zip(self.__lanes, devs):
+                lane["_device"] = d
 
     # ---- setup -------------------------------------------------------------------------
     @property
@@ -166,8 +196,57 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self._device = default_device()
         return self._device
 
+    @property
+    def devices(self) -> list[torch.device]:
+        """The device entries (multi-device mode), or the one device."""
+        return list(self.__multi_devices) if self.__multi_devices is not None else [self.device]
+
+    def _select_lane(self, g: int) -> None:
+        """Make device entry g's wave, ingest and device the current ones (multi-device mode)."""
+        if g == self.__lane:
+            return
+        cur = self.__lanes[self.__lane]
+        for a in _LANE_ATTRS:
+            cur[a] = getattr(self, a)
+        for a, v in self.__lanes[g].items():
+            setattr(self, a, v)
+        self.__lane = g
+
+    def _lane_for(self, worker_data: Any) -> int:
+        """The entry of an arrival: an update resident on a GPU goes to the entries of that GPU in
+        turn, any other update to all entries in turn; a round of per-element weights stays on the
+        first entry (its per-element totals are one arrival-order chain)."""
+        devs = self.__multi_devices
+        assert devs is not None
+        i = self.__arrivals
+        self.__arrivals += 1
+        if self.__ew:
+            return 0
+        payload = getattr(worker_data, "parameter", None) or getattr(worker_data, "delta_parameter", None)
+        first = next(iter(payload.values()), None) if isinstance(payload, dict) else None
+        if isinstance(first, torch.Tensor) and first.is_cuda:
+            on = [g for g, d in enumerate(devs) if d.index == first.get_device()]
+            if on:
+                return on[i % len(on)]
+        return i % len(devs)
+
+    def _multi(self) -> MultiDeviceContext:
+        assert self.__native_layout is not None and self.__multi_devices is not None
+        m = self.__multi
+        if m is None or m.layout != self.__native_layout:
+            if m is not None:
+                m.close()
+            m = self.__multi = MultiDeviceContext(self.__native_layout, self.__multi_devices)
+            if self.split_policy != 1:
+                for c in m.contexts:
+                    _native.check(c._lib.fedavg_set_split_policy(c._h, self.split_policy))
+            self.__ew_totals = None
+        return m
+
     def _context(self) -> FedAvgContext:
         assert self.__native_layout is not None
+        if self.__multi_devices is not None:
+            return self._multi().contexts[self.__lane]
         key = (self.device, self.__native_layout, self.split_policy)
         if self.__ctx is None or self.__ctx_key != key:
             if self.__ctx is not None:
@@ -184,6 +263,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _grow_layout(self, unknown: list[str], row: dict[str, tuple[Any, Any]]) -> None:
         """Names first seen in a later client (fed_avg_algorithm.py:55-62): append them to the
         layout, moving what is accumulated so far into a context of the grown layout."""
+        if self.__multi_devices is not None:
+            self._grow_layout_multi(unknown, row)
+            return
         self._flush()
         old_layout, old_native, old_ctx = self.__layout, self.__native_layout, self.__ctx
         assert old_layout is not None
@@ -212,6 +294,44 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             totals[k], valid[k] = old_totals[j], 1
         new_ctx.set_segment_state(totals, valid)
 
+    def _grow_layout_multi(self, unknown: list[str], row: dict[str, tuple[Any, Any]]) -> None:
+        """_grow_layout for every device entry: each entry's folded segments move into the grown
+        layout's context of the same entry."""
+        here = self.__lane
+        for g in range(len(self.__lanes)):
+            self._select_lane(g)
+            self._flush()
+        self._select_lane(here)
+        old_layout, old_native, old_multi = self.__layout, self.__native_layout, self.__multi
+        assert old_layout is not None
+        old_state = None
+        if old_multi is not None and old_native is not None and old_multi.layout == old_native:
+            # what each entry's context holds, read before the object is replaced
+            old_state = [([c.segment_offset(j) for j in range(old_native.num_segments)], *c.segment_state(),
+                          c.accumulator) for c in old_multi.contexts]
+        self.__layout = ModelLayout(names=old_layout.names + tuple(unknown),
+                                    shapes=old_layout.shapes + tuple(tuple(row[k][0].shape) for k in unknown))
+        self.__native_layout, self.__keep = split_empty(self.__layout)
+        for lane in self.__lanes:
+            lane["_FedAVGAlgorithm__base"] = None
+        self.__base = None
+        if old_state is None or self.__native_layout is None:
+            return
+        new_multi = self._multi()  # closes the old object (its accumulators stay alive here)
+        index = {n: i for i, n in enumerate(self.__native_layout.names)}
+        for g, (old_offs, old_totals, old_valid, old_acc) in enumerate(old_state):
+            new_ctx = new_multi.contexts[g]
+            totals = [0.0] * self.__native_layout.num_segments
+            valid = [0] * self.__native_layout.num_segments
+            for j, (name, n) in enumerate(zip(old_native.names, old_native.numels)):
+                k = index[name]
+                if not old_valid[j]:
+                    continue  # this entry never folded the segment
+                src, dst = old_offs[j], new_ctx.segment_offset(k)
+                new_ctx.accumulator[dst : dst + n].copy_(old_acc[src : src + n])
+                totals[k], valid[k] = old_totals[j], 1
+            new_ctx.set_segment_state(totals, valid)
+
     # ---- per arrival (fed_avg_algorithm.py:20-41) --------------------------------------
     def process_worker_data(
         self,
@@ -224,6 +344,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_data = self._all_worker_data.get(worker_id, None)
         if worker_data is None:
             return True
+        if self.__multi_devices is not None and self.accumulate:
+            self._select_lane(self._lane_for(worker_data))
         # messages are recognised by their dataclass fields, not by class identity: the
         # reference's own server passes simulation_lib.message objects (message.py)
         kind = message_kind(worker_data)
@@ -236,6 +358,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             assert len(worker_data.delta_parameter) == len(self._old_parameter)
             if self.__layout is None:
                 self._set_layout(self._old_parameter)
+            # a delta stages against the current layout: a later full update of this round must
+            # not replace it (its names are matched by name, new ones grow the layout)
+            self.__round_fresh = False
             w = worker_data.aggregation_weight
             if self.__default_hooks and isinstance(w, (int, float)) and \
                     self._stage_natively(worker_data.delta_parameter, w, delta=True):
@@ -258,10 +383,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 return True
         if kind != KIND_PARAMETER:
             return True
-        if self.__round_fresh and self.accumulate:
+        if self.__round_fresh and self.accumulate and not self.__has_data:
             # the reference's per-name dicts start empty every round (:55-62): the round's first
             # update sets the names and their order (a layout equal to the last round's keeps its
-            # context); later names grow it (_grow_layout)
+            # context); later names grow it (_grow_layout). Only while nothing is staged: staged
+            # rows and folded waves are laid out in the current layout.
             self.__round_fresh = False
             params = worker_data.parameter
             if isinstance(params, dict) and params and (self.__layout is None or tuple(params) != self.__layout.names):
@@ -431,6 +557,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def set_old_parameter(self, old_parameter: ModelParameter) -> None:
         if old_parameter is not self._old_parameter:
             self.__base = None
+            for lane in self.__lanes:
+                lane["_FedAVGAlgorithm__base"] = None
         super().set_old_parameter(old_parameter)
 
     def _delta_base(self) -> OutputTable:
@@ -742,6 +870,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return out
 
     def _reset_round(self) -> None:
+        self.__arrivals = 0
         self.__has_data = False
         self.__host_totals = {}
         self.__uniform_total, self.__uniform_count = None, 0
@@ -770,6 +899,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return moved
 
     def _finish_native(self) -> ModelParameter:
+        if self.__multi_devices is not None:
+            if not self.__ew:
+                return self._finish_multi()
+            self._select_lane(0)  # a round of per-element weights lives on the first entry
         ctx = self._context()
         native = self.__native_layout
         layout = self.__layout
@@ -853,6 +986,62 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         ctx.reset()
         return result
 
+    def _finish_multi(self) -> ModelParameter:
+        """The end of a multi-device round: every entry folds its last wave into its accumulator
+        (its shard's arrival-order partial), then the partials are summed in entry order on the
+        GPUs and divided by the round's arrival-order totals into the first entry's device
+        (``MultiDeviceContext.combine``), with the reference's NaN assertions."""
+        native, layout = self.__native_layout, self.__layout
+        assert native is not None and layout is not None
+        pending: list[list[tuple[ClientTable, Any]]] = []
+        for g in range(len(self.__lanes)):
+            self._select_lane(g)
+            table, dt = self.__table, self.__table_dtype
+            pending.append([(table, dt)] if table is not None and dt is not None else [])
+            self._flush()
+        self._select_lane(0)
+        m = self._multi()
+        custom_divide = type(self)._apply_total_weight is not FedAVGAlgorithm._apply_total_weight
+        if custom_divide:
+            totals = [1.0] * native.num_segments  # x / 1.0 == x: the hook divides on the host
+        elif self.__uniform_count and not self.__host_totals:
+            totals = [float(self.__uniform_total)] * native.num_segments
+        else:
+            self._materialize_totals()
+            totals = [float(self.__host_totals[layout.names[i]]) for i in self.__keep]
+        out_dtype = torch.float64 if custom_divide else self.result_dtype
+        offs, total, shapes = self._result_geometry(out_dtype)
+        flat = torch.empty(total, dtype=out_dtype, device=self.device)
+        self.__result_flat = None if custom_divide else flat
+        outs = OutputTable.from_flat(flat, offs, native)
+        try:
+            m.combine(totals, outs, out_dtype, root=0, exchange=self.exchange)
+        except Exception:
+            m.reset()
+            raise
+        m.raise_on_nan(pending)  # the round ends on the host: :35 / :93 / :97 asserted
+        result: ModelParameter = {}
+        if not custom_divide:
+            ext = _staging.module()
+            views = ext.views(flat, offs, shapes) if ext is not None else \
+                [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+            for j, i in enumerate(self.__keep):
+                result[layout.names[i]] = views[j]
+            return result
+        host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+        host.copy_(flat)
+        self._materialize_totals()
+        for j, i in enumerate(self.__keep):
+            name = layout.names[i]
+            tot = self._total_for(name, j)
+            if isinstance(tot, torch.Tensor):
+                tot = tot.cpu()
+            value = host[offs[j] : offs[j] + native.numels[j]].view(layout.shapes[i])
+            value = self._apply_total_weight(name=name, parameter=value, total_weight=tot)
+            assert not value.isnan().any()  # fed_avg_algorithm.py:97
+            result[name] = value.to(device=self.device, dtype=self.result_dtype)
+        return result
+
     def _result_geometry(self, out_dtype: torch.dtype) -> tuple[list[int], int, list[tuple[int, ...]]]:
         """(element offsets, flat size, shapes) of the native segments in a flat result buffer of
         ``out_dtype`` — cached per layout, reused every round."""
@@ -895,16 +1084,26 @@ class FedAVGAlgorithm(AggregationAlgorithm):
 
     def clear_worker_data(self) -> None:
         super().clear_worker_data()
+        for g in range(len(self.__lanes)):
+            self._select_lane(g)
+            self.__table, self.__table_dtype = None, None
+        if self.__lanes:
+            self._select_lane(0)
         self.__table, self.__table_dtype = None, None
         self.__row = {}
         self._reset_round()
         if self.__ctx is not None:
             self.__ctx.reset()
+        if self.__multi is not None:
+            self.__multi.reset()
 
     def exit(self) -> None:
         if self.__ctx is not None:
             self.__ctx.close()
             self.__ctx = None
+        if self.__multi is not None:
+            self.__multi.close()
+            self.__multi = None
 
     @classmethod
     def __aggregate_loss(cls, all_worker_data: MutableMapping[int, Message]) -> dict[str, Any]:

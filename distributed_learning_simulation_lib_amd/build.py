@@ -20,10 +20,11 @@ LIB_DIR = PKG_DIR / "_lib"
 LIB_NAME = "libfedavg_hip.so"
 LIB_PATH = LIB_DIR / LIB_NAME
 SOURCES = [CSRC / "fedavg_kernels.hip", CSRC / "personalized_kernels.hip", CSRC / "host_pack.cpp",
-           CSRC / "sharded_comm.cpp"]
-HEADERS = [REPO_DIR / "include" / "fedavg_hip.h", CSRC / "exact_div.h"]
+           CSRC / "sharded_comm.cpp", CSRC / "multi_device.cpp"]
+HEADERS = [REPO_DIR / "include" / "fedavg_hip.h", CSRC / "exact_div.h", CSRC / "rccl_bind.h"]
 # C++ clients of the ABI alone (no Python, no torch), built next to the library
 EXAMPLES = {"c_abi_round": REPO_DIR / "examples" / "c_abi_round.cpp",
+            "multi_device_round": REPO_DIR / "examples" / "multi_device_round.cpp",
             # test infrastructure: the native multi-rank round with ranks as threads on one GPU
             "threaded_ranks": REPO_DIR / "tests" / "native" / "threaded_ranks.cpp"}
 # test infrastructure: in-process RCCL stand-ins for threaded_ranks (tests/native/fake_rccl.cpp),
@@ -135,7 +136,8 @@ def build_examples(verbose: bool = False) -> list[Path]:
         if exe.exists() and exe.stat().st_mtime > max(src.stat().st_mtime, LIB_PATH.stat().st_mtime):
             built.append(exe)
             continue
-        _run([hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", f"-I{REPO_DIR / 'include'}", str(src),
+        _run([hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off", f"-I{REPO_DIR / 'include'}",
+              str(src),
               f"-L{LIB_DIR}", "-lfedavg_hip", "-pthread", "-Wl,-rpath,$ORIGIN", "-o", str(exe)], src.name, verbose)
         built.append(exe)
     return built

@@ -1799,6 +1799,82 @@ __global__ __launch_bounds__(kThreads) void copy_out_kernel(const TileDesc* __re
   if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) raise_flag(flag, 1);
 }
 
+// ---------------------------------------------------------------------------------------
+// Single-process multi-device exchange (multi_device.cpp, include/fedavg_hip.h fedavg_multi_*).
+// Device j owns a window of tiles; the partial kernels of every device wrote their fp64 partial
+// of that window into device j's receive slots (peer stores over xGMI) or left it in their own
+// accumulators (read here through the peer mapping). One workgroup per tile sums the G partials
+// in device order — S = S_0; S = S + S_1; ... — divides by the segment's total weight
+// (fed_avg_algorithm.py:71-99: the :93 / :97 NaN checks fused) and stores the result into the
+// root's outputs, which on a non-root device is a peer store. 256 lanes x 8 fp64 pairs: one
+// wave instruction moves 1 KiB of a slot contiguously.
+// ---------------------------------------------------------------------------------------
+constexpr int kMaxDevices = 16;
+struct SlotPtrs {
+  const double* p[kMaxDevices];
+};
+constexpr int kCombinePairs = 8;  // f64x2 per lane: 256 lanes x 16 elements = one 4096-element tile
+static_assert(kCombinePairs * 2 * kThreads == kTile1, "one workgroup per exact-order tile");
+
+template <typename O, bool VEC>
+__global__ __launch_bounds__(kThreads) void multi_combine_kernel(const TileDesc* __restrict__ tiles, int32_t tile_begin,
+                                                                 const SegDesc* __restrict__ segs, SlotPtrs slots,
+                                                                 int32_t G, const double* wtot, void* const* outs,
+                                                                 uint32_t* flag) {
+  const TileDesc td = load_tile(tiles, tile_begin + static_cast<int64_t>(blockIdx.x));
+  const int64_t base = to_const<int64_t>(segs)[2 * td.seg] + td.start;  // SegDesc::acc_off
+  const int li = static_cast<int>(threadIdx.x);
+  double acc[2 * kCombinePairs];
+#pragma unroll
+  for (int i = 0; i < 2 * kCombinePairs; ++i) acc[i] = 0.0;
+  const bool full = td.count == kCombinePairs * 2 * kThreads;
+  for (int g = 0; g < G; ++g) {
+    const gptr<const double> sp = to_global<double>(slots.p[g] + base);
+    double x[2 * kCombinePairs];
+#pragma unroll
+    for (int v = 0; v < kCombinePairs; ++v) {
+      const int e = (v * kThreads + li) * 2;
+      if (full || e + 2 <= td.count) {
+        const f64x2 d = __builtin_nontemporal_load((gptr<const f64x2>)(sp + e));
+        x[2 * v] = d.x;
+        x[2 * v + 1] = d.y;
+      } else {
+        x[2 * v] = (e < td.count) ? sp[e] : 0.0;
+        x[2 * v + 1] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * kCombinePairs; ++i) acc[i] = (g == 0) ? x[i] : acc[i] + x[i];
+  }
+  double res[2 * kCombinePairs];
+  exact_div_block<2 * kCombinePairs>(acc, res, to_const<double>(wtot)[td.seg]);
+  bool bad_acc = false, bad_res = false;
+  void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(outs)[td.seg]);
+  const gptr<O> op = to_global_mut<O>(out_raw) + td.start;
+#pragma unroll
+  for (int v = 0; v < kCombinePairs; ++v) {
+    const int e = (v * kThreads + li) * 2;
+    const bool in0 = full || e < td.count, in1 = full || e + 1 < td.count;
+    bad_acc |= (in0 && acc[2 * v] != acc[2 * v]) || (in1 && acc[2 * v + 1] != acc[2 * v + 1]);
+    bad_res |= (in0 && res[2 * v] != res[2 * v]) || (in1 && res[2 * v + 1] != res[2 * v + 1]);
+    if (VEC && in1) {
+      if constexpr (sizeof(O) == 4) {
+        store_out((gptr<f32x2>)(op + e), f32x2{static_cast<float>(res[2 * v]), static_cast<float>(res[2 * v + 1])});
+      } else {
+        store_out((gptr<f64x2>)(op + e), f64x2{res[2 * v], res[2 * v + 1]});
+      }
+    } else {
+      if (in0) op[e] = static_cast<O>(res[2 * v]);
+      if (in1) op[e + 1] = static_cast<O>(res[2 * v + 1]);
+    }
+  }
+  const uint64_t ba = __ballot(bad_acc), br = __ballot(bad_res);
+  if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+    if (ba) raise_flag(flag, 0);
+    if (br) raise_flag(flag, 1);
+  }
+}
+
 }  // namespace
 
 // =======================================================================================
@@ -2297,12 +2373,14 @@ int choose_split(const fedavg_ctx* c, int kmax) {
 // profiling is on, the profiling stop event is handed back in its place.
 int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_dtype, int out_kind,
                     int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1,
-                    hipEvent_t* done_ev = nullptr) {
+                    hipEvent_t* done_ev = nullptr, double* acc_out = nullptr) {
   if (st.delta) split = 1;  // delta folds run the exact-order kernel only
   KArgs a;
   a.segs = c->d_segs;
   a.tab = st.tab;
-  a.acc = c->acc;
+  // acc_out: a zero-initialised partial written elsewhere in accumulator coordinates (the
+  // multi-device exchange: another device's receive slot, through the peer mapping)
+  a.acc = acc_out ? acc_out : c->acc;
   a.flag = c->d_flag;
   a.K = st.stride;
   a.zero_init = zero_init;
@@ -3192,6 +3270,15 @@ int32_t fedavg_set_segment_state(fedavg_ctx* c, const double* total_weights, con
   return FEDAVG_OK;
 }
 
+int32_t fedavg_segment_state(const fedavg_ctx* c, double* total_weights, int32_t* valid) {
+  FEDAVG_RET(check_ctx(c));
+  for (int t = 0; t < c->T; ++t) {
+    if (total_weights) total_weights[t] = c->wsum[t];
+    if (valid) valid[t] = c->valid[t];
+  }
+  return FEDAVG_OK;
+}
+
 int32_t fedavg_accumulate_elementwise(fedavg_ctx* c, const void* const* client_ptrs, int32_t in_dtype,
                                       const void* const* weight_ptrs, const int32_t* weight_dtypes,
                                       const double* scalar_weights, const int32_t* total_fp32, int32_t K,
@@ -3371,6 +3458,88 @@ __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range(fed
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, p->zero_init, tb, te,
                      done_ev);
+}
+
+// Shared with multi_device.cpp: a zero-initialised partial plan's range launch that writes its fp64
+// partial into `acc_out` (accumulator coordinates; a peer device's receive slot) instead of the
+// context's accumulator. `done_ev` (optional) completes with the kernel.
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range_to(fedavg_plan* p, int32_t tb, int32_t te,
+                                                                              void* stream, double* acc_out) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind != fedavg_plan::PARTIAL || !p->zero_init)
+    return fail(FEDAVG_ERR_INVALID, "the multi-device exchange takes zero-initialised partial plans");
+  fedavg_ctx* c = p->ctx;
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, 1, tb, te, nullptr,
+                     acc_out);
+}
+
+// Shared with multi_device.cpp: the device-ordered sum of G fp64 partials over tiles [tb, te) of
+// the context's exact-order table, divided by wtot[seg] into outs[seg] (device tables of the
+// launching device), NaN flags into the context's words.
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_multi_combine(fedavg_ctx* c, int32_t tb, int32_t te,
+                                                                          const double* const* slots, int32_t G,
+                                                                          const double* wtot, void* const* outs,
+                                                                          int32_t out_dtype, int32_t vec, void* stream) {
+  if (!c) return fail(FEDAVG_ERR_INVALID, "null context");
+  if (G < 1 || G > kMaxDevices) return fail(FEDAVG_ERR_INVALID, "1 to 16 partials per combine");
+  const int32_t n = static_cast<int32_t>(c->tiles1.size());
+  if (tb < 0 || tb > te || te > n) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  if (tb == te) return FEDAVG_OK;
+  SlotPtrs sp{};
+  for (int32_t g = 0; g < G; ++g) {
+    if (!slots[g] || reinterpret_cast<uintptr_t>(slots[g]) % 16)
+      return fail(FEDAVG_ERR_INVALID, "partial buffers must be 16-byte aligned");
+    sp.p[g] = slots[g];
+  }
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(te - tb)), block(kThreads);
+  if (out_dtype == FEDAVG_F32) {
+    if (vec) hipLaunchKernelGGL((multi_combine_kernel<float, true>), grid, block, 0, s, c->d_tiles1, tb, c->d_segs, sp, G, wtot, outs, c->d_flag);
+    else hipLaunchKernelGGL((multi_combine_kernel<float, false>), grid, block, 0, s, c->d_tiles1, tb, c->d_segs, sp, G, wtot, outs, c->d_flag);
+  } else if (out_dtype == FEDAVG_F64) {
+    if (vec) hipLaunchKernelGGL((multi_combine_kernel<double, true>), grid, block, 0, s, c->d_tiles1, tb, c->d_segs, sp, G, wtot, outs, c->d_flag);
+    else hipLaunchKernelGGL((multi_combine_kernel<double, false>), grid, block, 0, s, c->d_tiles1, tb, c->d_segs, sp, G, wtot, outs, c->d_flag);
+  } else {
+    return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  return FEDAVG_OK;
+}
+
+// Shared with multi_device.cpp: per-segment "accumulator holds data" flags (out[T]), the tile
+// range [*tb, *te) of one segment, and the host state reset of a finished round.
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_segment_valid(const fedavg_ctx* c, int32_t* out) {
+  if (!c || !out) return fail(FEDAVG_ERR_INVALID, "null argument");
+  for (int t = 0; t < c->T; ++t) out[t] = c->valid[t];
+  return FEDAVG_OK;
+}
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_segment_tiles(const fedavg_ctx* c, int32_t seg,
+                                                                          int32_t* tb, int32_t* te) {
+  if (!c || seg < 0 || seg >= c->T || !tb || !te) return fail(FEDAVG_ERR_INVALID, "bad segment");
+  int32_t b = -1, e = -1;
+  for (int32_t i = 0; i < static_cast<int32_t>(c->tiles1.size()); ++i)
+    if (c->tiles1[i].seg == seg) {
+      if (b < 0) b = i;
+      e = i + 1;
+    }
+  *tb = b;
+  *te = e;
+  return FEDAVG_OK;
+}
+__attribute__((visibility("hidden"))) void fedavg_internal_clear_state(fedavg_ctx* c) {
+  std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
+  std::fill(c->valid.begin(), c->valid.end(), 0);
+}
+__attribute__((visibility("hidden"))) uint32_t fedavg_internal_flags(fedavg_ctx* c, int32_t clear) {
+  const uint32_t f = (__atomic_load_n(&c->h_flag[0], __ATOMIC_ACQUIRE) ? FEDAVG_FLAG_ACC_NAN : 0u) |
+                     (__atomic_load_n(&c->h_flag[1], __ATOMIC_ACQUIRE) ? FEDAVG_FLAG_RESULT_NAN : 0u);
+  if (clear)
+    for (int i = 0; i < 4; ++i) __atomic_store_n(&c->h_flag[i], 0u, __ATOMIC_RELEASE);
+  return f;
 }
 
 int32_t fedavg_plan_run_range(fedavg_plan* p, int32_t tb, int32_t te, void* stream) {

@@ -29,48 +29,32 @@
 #include <vector>
 
 #include "../../include/fedavg_hip.h"
+#include "rccl_bind.h"
 
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_fail(int32_t code, const char* msg);
 extern "C" __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range(
     fedavg_plan* p, int32_t tb, int32_t te, void* stream, hipEvent_t* done_ev);
 extern "C" __attribute__((visibility("hidden"))) int32_t fedavg_internal_set_prof(fedavg_ctx* c, int32_t on);
 
-namespace {
-
-struct Rccl {
-  void* handle = nullptr;
-  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
-  decltype(&ncclCommDestroy) comm_destroy = nullptr;
-  decltype(&ncclReduce) reduce = nullptr;
-  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
-  decltype(&ncclGroupStart) group_start = nullptr;
-  decltype(&ncclGroupEnd) group_end = nullptr;
-  decltype(&ncclGather) gather = nullptr;  // RCCL extension; grouped send / recv when absent
-  decltype(&ncclSend) send = nullptr;
-  decltype(&ncclRecv) recv = nullptr;
-  decltype(&ncclGetErrorString) error_string = nullptr;
-  std::string error;
-};
-
-// The process's RCCL, bound once. RTLD_NOLOAD first: if torch (or the caller) has loaded an RCCL,
-// use that very library, so one process never carries two RCCL runtimes.
-Rccl& rccl() {
-  static Rccl r;
+// The process's RCCL, bound once. FEDAVG_RCCL_LIB (a test stand-in) is loaded as named; otherwise
+// RTLD_NOLOAD first: if torch (or the caller) has loaded an RCCL, use that very library, so one
+// process never carries two RCCL runtimes.
+FedavgRccl& fedavg_rccl() {
+  static FedavgRccl r;
   static std::once_flag once;
   std::call_once(once, [] {
     const char* env = std::getenv("FEDAVG_RCCL_LIB");
-    const char* names[] = {env, "librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
-    for (const char* n : names) {
-      if (!n || !*n) continue;
-      r.handle = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
-      if (r.handle) break;
-    }
-    if (!r.handle) {
+    if (env && *env) {
+      r.handle = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
       for (const char* n : names) {
-        if (!n || !*n) continue;
-        r.handle = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+        r.handle = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
         if (r.handle) break;
+      }
+      for (const char* n : names) {
+        if (r.handle) break;
+        r.handle = dlopen(n, RTLD_NOW | RTLD_LOCAL);
       }
     }
     if (!r.handle) {
@@ -78,17 +62,19 @@ Rccl& rccl() {
       r.error = std::string("cannot load RCCL: ") + (e ? e : "not found");
       return;
     }
-    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(r.handle, "ncclGetUniqueId"));
-    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(r.handle, "ncclCommInitRank"));
-    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.handle, "ncclCommDestroy"));
-    r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(r.handle, "ncclReduce"));
-    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.handle, "ncclGetErrorString"));
-    r.reduce_scatter = reinterpret_cast<decltype(r.reduce_scatter)>(dlsym(r.handle, "ncclReduceScatter"));
-    r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(r.handle, "ncclGroupStart"));
-    r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(r.handle, "ncclGroupEnd"));
-    r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(r.handle, "ncclGather"));
-    r.send = reinterpret_cast<decltype(r.send)>(dlsym(r.handle, "ncclSend"));
-    r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(r.handle, "ncclRecv"));
+    auto sym = [](const char* name) { return dlsym(r.handle, name); };
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(sym("ncclCommInitRank"));
+    r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(sym("ncclCommInitAll"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(sym("ncclCommDestroy"));
+    r.reduce = reinterpret_cast<decltype(r.reduce)>(sym("ncclReduce"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+    r.reduce_scatter = reinterpret_cast<decltype(r.reduce_scatter)>(sym("ncclReduceScatter"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
+    r.gather = reinterpret_cast<decltype(r.gather)>(sym("ncclGather"));
+    r.send = reinterpret_cast<decltype(r.send)>(sym("ncclSend"));
+    r.recv = reinterpret_cast<decltype(r.recv)>(sym("ncclRecv"));
     if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.reduce || !r.error_string ||
         !r.reduce_scatter || !r.group_start || !r.group_end || !r.send || !r.recv)
       r.error = "RCCL library lacks a required symbol";
@@ -96,16 +82,23 @@ Rccl& rccl() {
   return r;
 }
 
-int32_t rccl_ready() {
-  Rccl& r = rccl();
+int32_t fedavg_rccl_ready() {
+  FedavgRccl& r = fedavg_rccl();
   if (!r.error.empty()) return fedavg_internal_fail(FEDAVG_ERR_RCCL, r.error.c_str());
   return FEDAVG_OK;
 }
 
-int32_t rccl_fail(ncclResult_t res, const char* what) {
-  std::string m = std::string(what) + ": " + rccl().error_string(res);
+int32_t fedavg_rccl_fail(ncclResult_t res, const char* what) {
+  std::string m = std::string(what) + ": " + fedavg_rccl().error_string(res);
   return fedavg_internal_fail(FEDAVG_ERR_RCCL, m.c_str());
 }
+
+namespace {
+
+using Rccl = FedavgRccl;
+Rccl& rccl() { return fedavg_rccl(); }
+int32_t rccl_ready() { return fedavg_rccl_ready(); }
+int32_t rccl_fail(ncclResult_t res, const char* what) { return fedavg_rccl_fail(res, what); }
 
 #define COMM_HIP_TRY(expr)                                                                          \
   do {                                                                                              \

@@ -334,6 +334,20 @@ class FedAvgContext:
         if split_policy is not None:
             _native.check(self._lib.fedavg_set_split_policy(self._h, split_policy))
 
+    @classmethod
+    def borrowed(cls, lib: ctypes.CDLL, handle: int, layout: ModelLayout, device: torch.device,
+                 accumulator: torch.Tensor) -> FedAvgContext:
+        """A view of a native context owned by another object (a device entry of
+        ``multi_device.MultiDeviceContext``): same methods, but ``close`` leaves it alone."""
+        self = cls.__new__(cls)
+        self._lib = lib
+        self.device = device
+        self.layout = layout
+        self.accumulator = accumulator
+        self._h = ctypes.c_void_p(handle)
+        self._borrowed = True
+        return self
+
     @staticmethod
     def _padded_acc_numel(layout: ModelLayout, lib: ctypes.CDLL) -> int:
         """Accumulator elements: every segment starts at a multiple of FEDAVG_ACC_ALIGN (32)."""
@@ -349,6 +363,9 @@ class FedAvgContext:
 
     # -- lifecycle -------------------------------------------------------------------
     def close(self) -> None:
+        if getattr(self, "_borrowed", False):
+            self._h = ctypes.c_void_p()  # the owner destroys it
+            return
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.fedavg_ctx_destroy(self._h)
             self._h = ctypes.c_void_p()
@@ -507,6 +524,14 @@ class FedAvgContext:
                 w.ctypes.data_as(_DBL), n, 1 if zero_init else 0, tile_begin, tile_end, self.stream,
             )
         )
+
+    def segment_state(self) -> tuple[list[float], list[int]]:
+        """(per-segment total weight, 1 = the accumulator holds folded data) — what
+        ``set_segment_state`` sets."""
+        tw = (ctypes.c_double * self.layout.num_segments)()
+        vv = (ctypes.c_int32 * self.layout.num_segments)()
+        _native.check(self._lib.fedavg_segment_state(self._h, tw, vv))
+        return list(tw), list(vv)
 
     def set_segment_state(self, total_weights: Sequence[float], valid: Sequence[int]) -> None:
         """Per-segment accumulated state (a layout grown mid-round keeps its folded segments)."""

@@ -489,10 +489,14 @@ def sharded_reduce(
         # exchange each rank's window finalize too) are OR-ed across ranks before anyone raises,
         # so no rank returns normally and then waits in the next round's collectives
         dev = acc.device if acc.is_cuda and not host_staged else None
-        flags = union_flags(reducer.nan_flags(), group, dev)
+        local = reducer.nan_flags()
+        flags = union_flags(local, group, dev)
         if flags:
-            if rank == root:
-                reducer.raise_on_nan()  # the reference's stage, naming the root's own clients
+            if rank == root or local:
+                # the reference's stage from this rank's own flags: a rank whose shard holds the
+                # NaN input scans its own tables and names its clients (:35); the root names the
+                # stage of its finalize (:93 / :97)
+                reducer.raise_on_nan()
             raise_for_flags(flags, f"reported by the sharded round on rank {rank}")
     return global_totals
 

@@ -282,6 +282,9 @@ int32_t fedavg_plan_run_range(fedavg_plan* plan, int32_t tile_begin, int32_t til
  * makes the next fold of that segment an assignment.
  */
 int32_t fedavg_set_segment_state(fedavg_ctx* ctx, const double* total_weights, const int32_t* valid);
+/* The reverse: per segment the host total weight so far and whether the accumulator holds data
+ * (total_weights[num_segments], valid[num_segments]; either may be NULL). */
+int32_t fedavg_segment_state(const fedavg_ctx* ctx, double* total_weights, int32_t* valid);
 
 /*
  * Per-element weights (a _get_weight override returning a tensor of the parameter's shape,
@@ -441,6 +444,65 @@ int32_t fedavg_sharded_round_scatter(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_
 int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_plan* partial, fedavg_plan* finalize,
                                    const int32_t* tile_edges, int32_t num_edges, int32_t exchange, int32_t root,
                                    void* stream);
+
+/* =====================================================================================
+ * Single-process multi-device mode ("a communicator created by the library
+ * from a device list"). The reference drives aggregation from ONE server process
+ * (simulation_lib/server/server.py:122-152 -> aggregation_server.py:111-145 ->
+ * FedAVGAlgorithm.process_worker_data / aggregate_worker_data, fed_avg_algorithm.py:20-113);
+ * this object lets that one process shard the sum of fed_avg_algorithm.py:43-64 over G MI355X.
+ *
+ *   fedavg_multi_create(&m, devices, G, seg_numel, T, accumulators_or_NULL)
+ *       one context per device entry (fedavg_multi_context: fold that device's shard with the
+ *       single-device calls above), one library stream and one high-priority exchange stream per
+ *       entry, peer access enabled between distinct devices (fedavg_multi_peer_access). Entries
+ *       may repeat a device (aliased devices: tests on one GPU).
+ *   fedavg_multi_round(m, partials[G], totals, outs, out_dtype, root, edges, n_edges, exchange,
+ *                      streams)
+ *       one round of device-resident clients: partials[g] is a zero-initialised partial plan on
+ *       context g (NULL = device g holds no client). Exchanges:
+ *        FEDAVG_EXCHANGE_PEER  — chunk k (tiles [edges[k], edges[k+1])) is cut into G windows,
+ *          device j owns window j. Device g's partial kernel for window j stores its fp64 partial
+ *          straight into device j's receive slot over xGMI (own window last); device j then sums
+ *          the G partials of its window in device order S_0 + S_1 + ... (deterministic),
+ *          divides by totals[t] and stores the result into the root's outputs (a peer store).
+ *          Cross-device order is carried by events (no spinning kernel). Needs peer access
+ *          (or aliased devices).
+ *        FEDAVG_EXCHANGE_REDUCE — each chunk's partials are reduced to the root's accumulator by
+ *          an in-process RCCL communicator (ncclCommInitAll, created on first use; RCCL's
+ *          summation order), then the root divides.
+ *       streams[g]: the caller's stream of entry g (NULL = the library's); each entry's work is
+ *       ordered after what the caller enqueued there before, and streams[root] is ordered after
+ *       the whole round.
+ *   fedavg_multi_combine(m, totals, outs, out_dtype, root, exchange, streams)
+ *       the streaming form: every context's accumulator already holds its shard's fp64 partial
+ *       (folded in waves with fedavg_accumulate on context g); segments a context never folded
+ *       count as the identity. FEDAVG_ERR_STATE if no context folded some segment (the :88
+ *       assertion). Resets every context's accumulated state (fed_avg_algorithm.py:90,98).
+ *   fedavg_multi_check(m, flags_out): synchronise every stream of the object and report the OR
+ *       of every context's NaN flags like fedavg_check; fedavg_multi_reset clears them.
+ * Results: each device's fold is the exact arrival-order chain of its clients; PEER sums the
+ * partials in device order (bit-identical to that host composition), REDUCE in RCCL's order.
+ * ===================================================================================== */
+#define FEDAVG_EXCHANGE_PEER 2
+#define FEDAVG_MULTI_MAX_DEVICES 16
+typedef struct fedavg_multi fedavg_multi;
+int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t num_devices, const int64_t* seg_numel,
+                            int32_t num_segments, void* const* accumulators);
+int32_t fedavg_multi_destroy(fedavg_multi* m);
+int32_t fedavg_multi_num_devices(const fedavg_multi* m);
+int32_t fedavg_multi_device(const fedavg_multi* m, int32_t index);
+fedavg_ctx* fedavg_multi_context(fedavg_multi* m, int32_t index);
+void* fedavg_multi_stream(fedavg_multi* m, int32_t index);
+/* 1 when every pair of distinct devices of the object has peer access enabled, else 0 */
+int32_t fedavg_multi_peer_access(const fedavg_multi* m);
+int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const double* total_weights,
+                           void* const* out_ptrs, int32_t out_dtype, int32_t root, const int32_t* tile_edges,
+                           int32_t num_edges, int32_t exchange, void* const* streams);
+int32_t fedavg_multi_combine(fedavg_multi* m, const double* total_weights, void* const* out_ptrs, int32_t out_dtype,
+                             int32_t root, int32_t exchange, void* const* streams);
+int32_t fedavg_multi_check(fedavg_multi* m, uint32_t* flags_out);
+int32_t fedavg_multi_reset(fedavg_multi* m);
 
 #ifdef __cplusplus
 }

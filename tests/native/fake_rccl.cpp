@@ -12,6 +12,10 @@
 // ncclReduce (result on root), ncclReduceScatter (rank r gets window r), ncclGather (rank r's
 // buffer at recv + r * count on root; in place when send == that slot), ncclSend / ncclRecv
 // (paired through a mailbox, the gather fallback when built with -DFAKE_RCCL_NO_GATHER).
+// ncclCommInitAll makes the communicators of ONE host thread driving every rank (the single-process
+// multi-device mode, multi_device.cpp): their collectives must sit between ncclGroupStart and
+// ncclGroupEnd, are queued there, and run at the outermost ncclGroupEnd — the i-th call of every
+// rank forms one collective, summed in rank order like the threaded form.
 // Not the product: nothing outside tests/ loads it.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -106,7 +110,53 @@ bool sum_into(Group* g, ncclDataType_t t, size_t off, size_t count, void* dst, h
 struct ncclComm {
   Group* g;
   int rank;
+  bool single = false;  // made by ncclCommInitAll: one thread drives every rank
 };
+
+namespace {
+
+// grouped calls of single-thread communicators, queued until the outermost ncclGroupEnd
+struct Pending {
+  ncclComm_t comm;
+  const void* send;
+  void* recv;
+  size_t count;
+  ncclDataType_t dt;
+  int root;
+  hipStream_t stream;
+};
+thread_local int g_depth = 0;
+thread_local std::vector<Pending> g_pending;
+
+ncclResult_t run_pending() {
+  std::vector<Pending> ops;
+  ops.swap(g_pending);
+  // per communicator group: the i-th op of each rank forms collective i
+  std::map<Group*, std::vector<std::vector<Pending>>> by_group;
+  for (const Pending& p : ops) {
+    auto& ranks = by_group[p.comm->g];
+    ranks.resize(p.comm->g->n);
+    ranks[p.comm->rank].push_back(p);
+  }
+  for (auto& [g, ranks] : by_group) {
+    const size_t n_ops = ranks[0].size();
+    for (const auto& r : ranks)
+      if (r.size() != n_ops) return ncclInvalidUsage;  // every rank must join every collective
+    for (size_t i = 0; i < n_ops; ++i) {
+      for (int r = 0; r < g->n; ++r) {
+        const Pending& p = ranks[r][i];
+        if (hipStreamSynchronize(p.stream) != hipSuccess) return ncclUnhandledCudaError;
+        g->send[r] = p.send;
+        g->recv[r] = p.recv;
+      }
+      const Pending& rootp = ranks[ranks[0][i].root][i];
+      if (!sum_into(g, rootp.dt, 0, rootp.count, rootp.recv, rootp.stream)) return ncclInvalidArgument;
+    }
+  }
+  return ncclSuccess;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -160,12 +210,42 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
 
 const char* ncclGetErrorString(ncclResult_t) { return "fake rccl: collective failed"; }
 
-ncclResult_t ncclGroupStart() { return ncclSuccess; }
-ncclResult_t ncclGroupEnd() { return ncclSuccess; }
+ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
+  (void)devlist;  // duplicates welcome: every rank may sit on the one test GPU
+  if (!comms || ndev < 1) return ncclInvalidArgument;
+  Group* g = new Group();
+  g->n = ndev;
+  g->refs = ndev;
+  g->send.assign(ndev, nullptr);
+  g->recv.assign(ndev, nullptr);
+  g->box.assign(static_cast<size_t>(ndev) * ndev, nullptr);
+  g->box_count.assign(static_cast<size_t>(ndev) * ndev, 0);
+  {
+    std::lock_guard<std::mutex> lk(g_registry_mutex);
+    g_registry["fake-rccl-all-" + std::to_string(g_next_id++)] = g;
+  }
+  for (int r = 0; r < ndev; ++r) comms[r] = new ncclComm{g, r, true};
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGroupStart() {
+  ++g_depth;
+  return ncclSuccess;
+}
+ncclResult_t ncclGroupEnd() {
+  if (g_depth <= 0) return ncclInvalidUsage;
+  if (--g_depth == 0 && !g_pending.empty()) return run_pending();
+  return ncclSuccess;
+}
 
 ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype, ncclRedOp_t op,
                         int root, ncclComm_t comm, hipStream_t stream) {
   if (op != ncclSum || root < 0 || root >= comm->g->n) return ncclInvalidArgument;
+  if (comm->single) {
+    if (g_depth == 0) return ncclInvalidUsage;  // one thread, many ranks: grouped calls only
+    g_pending.push_back(Pending{comm, sendbuff, recvbuff, count, datatype, root, stream});
+    return ncclSuccess;
+  }
   if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
   Group* g = comm->g;
   g->send[comm->rank] = sendbuff;

@@ -84,6 +84,50 @@ def test_native_delta_staging_matches_python_staging(hip_device, monkeypatch):
         assert bits_equal(native[n].numpy(), python[n].numpy()), n
 
 
+@pytest.mark.parametrize("wave", [1, 64])
+@pytest.mark.parametrize("native", [True, False])
+def test_delta_first_round_then_reordered_full_update(hip_device, monkeypatch, wave, native):
+    # a round that opens with fused deltas keeps its layout when a later full update arrives with
+    # its keys in another order (ParameterMessage.complete appends the missing keys at the end,
+    # message.py:28-31): the deltas already staged or folded stay where they are
+    from distributed_learning_simulation_lib_amd.message import DeltaParameterMessage
+    from oracle.fedavg_oracle import complete, restore
+
+    if not native:
+        monkeypatch.setattr(_staging, "module", lambda: None)
+    g = torch.Generator().manual_seed(23)
+    old = {n: torch.randn(s, generator=g, dtype=torch.float64) for n, s in SHAPES.items()}
+    old_np = {n: t.numpy() for n, t in old.items()}
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=wave)
+    algo.set_old_parameter(old)
+    oracle = OracleFedAvg()
+    for rnd in range(2):  # the second round opens with a delta again, after a reset
+        for k in range(5):
+            if k in (0, 1, 3):
+                d = {n: torch.randn(s, generator=g) for n, s in SHAPES.items()}
+                algo.process_worker_data(k, DeltaParameterMessage(
+                    delta_parameter={n: t.to(hip_device) for n, t in d.items()}, aggregation_weight=50 + k))
+                full = restore({n: t.numpy() for n, t in d.items()}, old_np)
+            else:
+                part = {n: torch.randn(SHAPES[n], generator=g) for n in ("fc", "scalar", "conv")}
+                msg = ParameterMessage(parameter={n: t.to(hip_device) for n, t in part.items()},
+                                       aggregation_weight=70 + k)
+                msg.complete(old)  # appends "empty" and "bias" after the sent keys
+                assert list(msg.parameter)[:3] == ["fc", "scalar", "conv"]
+                algo.process_worker_data(k, msg)
+                full = {n: t.numpy() for n, t in part.items()}
+                complete(full, old_np)
+            oracle.process_worker_data(k, OracleMessage(parameter=full, aggregation_weight=(50 if k in (0, 1, 3)
+                                                                                              else 70) + k))
+        got = algo.aggregate_worker_data().parameter
+        want = oracle.aggregate_worker_data().parameter
+        assert list(got) == list(want) == list(SHAPES), rnd
+        for n, v in want.items():
+            assert bits_equal(got[n].cpu().numpy(), v), (rnd, n)
+        algo.clear_worker_data()
+        oracle = OracleFedAvg()
+
+
 @pytest.mark.parametrize("wave", [1, 3, 64])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
 def test_native_host_staging_bit_identical(hip_device, wave, dtype):

@@ -30,6 +30,16 @@ relays rank 0's single JSON line and exits non-zero if any rank fails or outlive
 ``--launch-timeout`` — the reference's simulator likewise starts its own worker processes
 (simulation_lib/task.py:142-185, context.py:215-230). Under ``torch.distributed.run`` (WORLD_SIZE
 set) the ranks are already there and nothing is spawned.
+
+Failing fast (the driver gives an N > 1 run 600 s): every rank of an N > 1 run records its stage
+(init, comm, tune, warmup, timed, ...) and a watchdog thread ends the rank with status 124 and the
+stage's name on stderr when one stage outlives its limit (``--stage-timeout``, default 150 s; the
+process group's own timeout is 120 s) — so under ``torch.distributed.run`` a hung collective ends
+the job in minutes with the stuck rank named. The self-launcher (default ``--launch-timeout``
+480 s) prints every rank's last stage when it stops a run, and when the ranks failed with the
+library's native RCCL communicator it starts ONE fresh set of rank processes with ``--comm torch``
+(the launcher never touched a GPU; no rank is re-executed); that line says so in
+``config.launch_fallback``.
 """
 
 from __future__ import annotations
@@ -39,6 +49,7 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 from pathlib import Path
 
 
@@ -50,6 +61,23 @@ def _free_port() -> int:
         return int(s.getsockname()[1])
 
 
+def _stage_report(status_dir: str | None, n: int, running: list[int]) -> str:
+    """One line per rank: its last recorded stage (BENCH_STATUS_DIR/rank<r>) and whether it runs."""
+    out = []
+    for r in range(n):
+        stage, age = "no stage recorded", None
+        if status_dir:
+            try:
+                p = Path(status_dir) / f"rank{r}"
+                stage = p.read_text().strip() or stage
+                age = time.time() - p.stat().st_mtime
+            except OSError:
+                pass
+        state = "still running" if r in running else "exited"
+        out.append(f"rank {r} {state}, last stage '{stage}'" + (f" ({age:.0f} s ago)" if age is not None else ""))
+    return "; ".join(out)
+
+
 def _launch_ranks(argv: list[str]) -> int | None:
     """Spawn the ranks of a ``--gpus N`` run when no launcher did (see the module docstring).
 
@@ -57,22 +85,50 @@ def _launch_ranks(argv: list[str]) -> int | None:
     (or a one-GPU run) and should go on to main(). Only the standard library is used here: the
     parent imports neither torch nor the package, so it never initialises the GPU and the
     children start from a clean process (no fork of a HIP runtime)."""
+    import tempfile
+
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--launch-timeout", type=float, default=480.0)
+    pre.add_argument("--comm", default="native")
+    pre.add_argument("--no-fallback", action="store_true")
+    pre.add_argument("--procs", type=int, default=0)
+    known, _ = pre.parse_known_args(argv)
+    if known.gpus <= 1 or "WORLD_SIZE" in os.environ or known.procs == 1:
+        return None
+    deadline = time.monotonic() + known.launch_timeout
+    status_dir = tempfile.mkdtemp(prefix="bench_status_")
+    rc, failed = _run_ranks(argv, known.gpus, deadline, known.launch_timeout, status_dir, None)
+    if rc != 0 and failed and known.comm == "native" and not known.no_fallback:
+        left = deadline - time.monotonic()
+        if left > 30.0:
+            print(f"bench.py launcher: retrying once with fresh rank processes and --comm torch "
+                  f"({left:.0f} s left)", file=sys.stderr)
+            rc, _ = _run_ranks([*argv, "--comm", "torch"], known.gpus, deadline, known.launch_timeout, status_dir,
+                               "native RCCL communicator run failed; this line is the --comm torch rerun")
+    return rc
+
+
+def _run_ranks(argv: list[str], n: int, deadline: float, budget: float, status_dir: str,
+               fallback_note: str | None) -> tuple[int, bool]:
+    """Spawn n rank processes of this script and wait for them (see _launch_ranks). Returns (exit
+    code, whether a rank failed or hung — the failures a --comm torch rerun may cure)."""
     import signal
     import subprocess
     import threading
 
-    pre = argparse.ArgumentParser(add_help=False)
-    pre.add_argument("--gpus", type=int, default=1)
-    pre.add_argument("--launch-timeout", type=float, default=1200.0)
-    known, _ = pre.parse_known_args(argv)
-    if known.gpus <= 1 or "WORLD_SIZE" in os.environ:
-        return None
-    n = known.gpus
     port = _free_port()
     procs: list[subprocess.Popen] = []
     base = dict(os.environ)
     base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                GROUP_RANK="0", BENCH_LAUNCHED_BY="bench.py")
+                GROUP_RANK="0", BENCH_LAUNCHED_BY="bench.py", BENCH_STATUS_DIR=status_dir)
+    if fallback_note:
+        base["BENCH_LAUNCH_FALLBACK"] = fallback_note
+    for r in range(n):
+        try:
+            (Path(status_dir) / f"rank{r}").unlink()
+        except OSError:
+            pass
     for r in range(n):
         env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen(
@@ -110,31 +166,34 @@ def _launch_ranks(argv: list[str]) -> int | None:
                     pass
                 p.wait()
 
-    deadline = time.monotonic() + known.launch_timeout
     failed = None
     while True:
         codes = [p.poll() for p in procs]
         bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
         if bad:
-            failed = f"rank {bad[0][0]} exited with status {bad[0][1]}"
+            time.sleep(0.5)  # ranks that fail because of the first (a peer left) are reported too
+            codes = [p.poll() for p in procs]
+            failed = "; ".join(f"rank {r} exited with status {c}" for r, c in enumerate(codes) if c not in (None, 0))
             break
         if all(c == 0 for c in codes):
             break
         if time.monotonic() > deadline:
-            failed = f"ranks still running after --launch-timeout {known.launch_timeout:g} s"
+            failed = f"ranks still running after --launch-timeout {budget:g} s"
             break
         time.sleep(0.2)
     if failed:
+        running = [r for r, p in enumerate(procs) if p.poll() is None]
+        report = _stage_report(status_dir, n, running)
         stop_all()
         reader.join(timeout=5.0)
-        print(f"bench.py launcher: {failed}; stopped all {n} ranks", file=sys.stderr)
-        return 1
+        print(f"bench.py launcher: {failed}; {report}; stopped all {n} ranks", file=sys.stderr)
+        return 1, True
     reader.join(timeout=30.0)
     if len(json_lines) != 1:
         print(f"bench.py launcher: rank 0 printed {len(json_lines)} JSON lines (expected 1)", file=sys.stderr)
-        return 1
+        return 1, False
     print(json_lines[0], flush=True)
-    return 0
+    return 0, False
 
 
 if __name__ == "__main__":
@@ -168,6 +227,55 @@ from distributed_learning_simulation_lib_amd.sharded import (  # noqa: E402
 )
 
 METRIC = "aggregated GB/s (device-resident), N-client weighted FedAvg reduce, 1/2/4/8 GPU"
+PG_TIMEOUT_S = 120  # torch.distributed process group timeout (its collectives and rendezvous)
+
+
+class _Stages:
+    """A rank's current stage of an N > 1 run: written to BENCH_STATUS_DIR/rank<r> (the
+    self-launcher's report when it stops a run) and watched by a daemon thread that ends the rank
+    with status 124 — naming the stage on stderr — when one stage outlives its limit, so a hung
+    collective cannot hold the run until the driver's kill. Test hook: BENCH_INJECT_HANG=
+    "<rank>:<stage>:<comm|any>" makes that rank sleep in that stage."""
+
+    def __init__(self) -> None:
+        self.rank, self.name, self.limit = 0, "start", 0.0
+        self.t = time.monotonic()
+        self.comm = "native"
+        self.status = None
+
+    def start(self, rank: int, default_limit: float, comm: str) -> None:
+        import threading
+
+        self.rank, self.default, self.comm = rank, default_limit, comm
+        d = os.environ.get("BENCH_STATUS_DIR")
+        self.status = Path(d) / f"rank{rank}" if d else None
+        if default_limit > 0:
+            threading.Thread(target=self._watch, daemon=True).start()
+
+    def enter(self, name: str, limit: float | None = None) -> None:
+        self.name, self.t = name, time.monotonic()
+        self.limit = self.default if limit is None else limit
+        if self.status is not None:
+            try:
+                self.status.write_text(name + "\n")
+            except OSError:
+                pass
+        hang = os.environ.get("BENCH_INJECT_HANG", "").split(":")
+        if len(hang) == 3 and hang[0] == str(self.rank) and hang[1] == name and hang[2] in ("any", self.comm):
+            print(f"bench.py rank {self.rank}: injected hang in stage '{name}'", file=sys.stderr, flush=True)
+            while True:
+                time.sleep(1.0)
+
+    def _watch(self) -> None:
+        while True:
+            time.sleep(0.5)
+            if self.limit > 0 and time.monotonic() - self.t > self.limit:
+                print(f"bench.py rank {self.rank}: stage '{self.name}' still running after {self.limit:g} s "
+                      f"(--stage-timeout); ending the rank", file=sys.stderr, flush=True)
+                os._exit(124)
+
+
+_STAGES = _Stages()
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -954,8 +1062,11 @@ def main_dry(args: argparse.Namespace) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
+        _STAGES.start(rank, args.stage_timeout, args.comm)
+        _STAGES.enter("init_process_group")
         _rendezvous_env()
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=PG_TIMEOUT_S))
+        _STAGES.enter("shards")
     layout = LAYOUTS[args.layout]()
     n_total = job_clients(args, world)
     lo, hi = shard_bounds(n_total, world, rank)
@@ -970,6 +1081,8 @@ def main_dry(args: argparse.Namespace) -> int:
         dist.barrier()
     else:
         gathered = [shards]
+    if world > 1:
+        _STAGES.enter("timed")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pass
@@ -993,6 +1106,8 @@ def main_dry(args: argparse.Namespace) -> int:
         "dry_run": "launcher check on the CPU: rank processes, gloo group, shards, max-over-ranks timing; "
                    "not a measurement",
     }
+    if os.environ.get("BENCH_LAUNCH_FALLBACK"):
+        line["config"]["launch_fallback"] = os.environ["BENCH_LAUNCH_FALLBACK"]
     print(json.dumps(line), flush=True)
     return 0
 
@@ -1048,9 +1163,22 @@ def main() -> int:
                          "gradient: GradientWorker's in-round rounds through the plugin, as a latency "
                          "(--clients-per-gpu default 8)")
     ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
-    ap.add_argument("--launch-timeout", type=float, default=1200.0,
+    ap.add_argument("--launch-timeout", type=float, default=480.0,
                     help="--gpus N > 1 without an external launcher: seconds before the spawned ranks are "
-                         "stopped and the run fails")
+                         "stopped and the run fails (one --comm torch rerun within the same budget)")
+    ap.add_argument("--no-fallback", action="store_true",
+                    help="self-launched N > 1: no --comm torch rerun after a failed native-communicator run")
+    ap.add_argument("--stage-timeout", type=float, default=150.0,
+                    help="N > 1: a rank whose current stage (init, comm, tune, warmup, timed, ...) runs longer "
+                         "ends with status 124, naming the stage (0 = no watchdog)")
+    ap.add_argument("--tune-budget", type=float, default=60.0,
+                    help="N > 1 with --exchange auto: seconds of exchange tuning before the best candidate "
+                         "timed so far is taken")
+    ap.add_argument("--procs", type=int, default=0,
+                    help="--procs 1 with --gpus N: one process drives the N GPUs (fedavg_multi_*, the "
+                         "single-process multi-device mode) instead of one rank process per GPU")
+    ap.add_argument("--multi-exchange", default="peer", choices=["peer", "reduce"],
+                    help="--procs 1: the peer-window exchange (no collective library) or the in-process RCCL reduce")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: every rank joins a gloo group, takes its client "
                          "shard and the max-over-ranks timing of an empty step; prints the JSON line "
@@ -1079,11 +1207,15 @@ def main() -> int:
     # --rehearse: every rank on cuda:0 over a gloo group (the exchange staged through host memory,
     # RCCL refuses two ranks on one GPU) — runs this N > 1 code path on a one-GPU box; its times
     # are not the N-GPU numbers
+    if world > 1:
+        _STAGES.start(rank, args.stage_timeout, args.comm)
+        _STAGES.enter("init_process_group")
     device = torch.device("cuda", 0 if args.rehearse else local_rank)
     torch.cuda.set_device(device)
+    pg_timeout = timedelta(seconds=PG_TIMEOUT_S)
     if args.rehearse and (world > 1 or args.force_collective):
         _rendezvous_env()
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout)
         args.comm = "torch"
     elif world > 1 or args.force_collective:
         _rendezvous_env()
@@ -1091,7 +1223,10 @@ def main() -> int:
         # chunk's partial-kernel workgroups, so the reduce of chunk c starts under chunk c+1
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
-        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world, pg_options=opts)
+        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world, pg_options=opts,
+                                timeout=pg_timeout)
+    if world > 1:
+        _STAGES.enter("make_clients")
     sharded = world > 1 or args.force_collective
     chunks_auto = args.chunks <= 0
     if chunks_auto:
@@ -1132,6 +1267,8 @@ def main() -> int:
     host_enqueue = [0.0]  # host time to enqueue one round (diagnostic: is the step host-bound?)
 
     comm = None
+    if world > 1:
+        _STAGES.enter("comm_create")
     if sharded and args.comm == "native":
         try:
             comm = RcclComm(device)
@@ -1155,9 +1292,12 @@ def main() -> int:
         # time every (exchange, chunks) candidate on this node before the warmup (untimed; the
         # max over ranks decides, so every rank picks the same): the link rate the DESIGN.md §5
         # cost model assumes is not measurable on one GPU
+        if world > 1:
+            _STAGES.enter("tune", args.tune_budget + args.stage_timeout)
         (exchange, args.chunks, chunk_shape), times = tune_exchange(
             reducer, local_totals, exchange_candidates(None if chunks_auto else args.chunks), rounds=3,
-            global_total_weights=global_totals, comm=comm, force_collective=args.force_collective)
+            global_total_weights=global_totals, comm=comm, force_collective=args.force_collective,
+            budget_s=args.tune_budget)
         tuned = {f"{e}/{c}/{sh}": round(ms, 4) for (e, c, sh), ms in times.items()}
         selection = "tuned"
 
@@ -1172,11 +1312,15 @@ def main() -> int:
         if rank == 0:
             reducer.raise_on_nan()
 
+    if world > 1:
+        _STAGES.enter("warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(device)
     if dist.is_initialized():
         dist.barrier()
+    if world > 1:
+        _STAGES.enter("timed")
     ctx.prof_collect()  # drop warmup events
     host_enqueue[0] = 0.0
     ctx.prof_enable(not args.no_kernel_events)
@@ -1232,6 +1376,8 @@ def main() -> int:
     # of the step is the exposed reduce tail + the root's finalize.
     partial_only_ms = None
     pplan = getattr(reducer, "_partial_plan", None) if sharded else None
+    if world > 1:
+        _STAGES.enter("partial_only")
     if pplan is not None:
         torch.cuda.synchronize(device)
         if dist.is_initialized():
@@ -1260,12 +1406,16 @@ def main() -> int:
         torch.cuda.empty_cache()
         cpu = cpu_baseline(layout)
 
+    if world > 1:
+        _STAGES.enter("teardown")
     if comm is not None:
         torch.cuda.synchronize(device)
         comm.close()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+    if world > 1:
+        _STAGES.enter("done", 0)
     if rank != 0:
         return 0
     workload = workload_name(args, world, n_total, n_waves, wave)
@@ -1322,6 +1472,8 @@ def main() -> int:
             "baseline_config": baseline_config,
             **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not an N-GPU measurement"}
                if args.rehearse else {}),
+            **({"launch_fallback": os.environ["BENCH_LAUNCH_FALLBACK"]} if os.environ.get("BENCH_LAUNCH_FALLBACK")
+               else {}),
         },
         "roofline": {
             "bound": "hbm",

@@ -523,6 +523,7 @@ def tune_exchange(
     comm: RcclComm | None = None,
     force_collective: bool = False,
     check_nan: bool = True,
+    budget_s: float | None = None,
 ) -> tuple[tuple[str, int, str], dict[tuple[str, int, str], float]]:
     """Pick the exchange, chunk count and chunk shape by timing the job itself.
 
@@ -534,8 +535,10 @@ def tune_exchange(
     with the root reading the NaN flags (``check_nan``): without that host sync, back-to-back
     rounds overlap one round's exchange with the next round's fold, a pipelining no
     round-by-round server gets, and the candidates would be ranked on it. Ties go to the earlier candidate.
-    Returns ``((exchange, chunks, shape), {candidate: ms per round})``. Collective: every rank of
-    ``group`` calls it with the same candidates.
+    ``budget_s``: once this many seconds of tuning have passed (the max over ranks, taken with each
+    candidate's time, so every rank stops after the same candidate) the rest are not timed.
+    Returns ``((exchange, chunks, shape), {candidate: ms per round})`` — the candidates timed.
+    Collective: every rank of ``group`` calls it with the same candidates.
     """
     cands = list(candidates) if candidates is not None else exchange_candidates()
     if not cands:
@@ -554,6 +557,7 @@ def tune_exchange(
             torch.cuda.synchronize(acc.device)
 
     times: dict[tuple[str, int, str], float] = {}
+    t_start = time.perf_counter()
     for ex, ch, sh in cands:
         kw = dict(chunks=ch, root=root, group=group, global_total_weights=global_total_weights,
                   force_collective=force_collective, comm=comm, exchange=ex, check_nan=check_nan, shape=sh)
@@ -564,11 +568,14 @@ def tune_exchange(
         for _ in range(max(1, rounds)):
             sharded_reduce(reducer, local_total_weights, **kw)
         settle()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                          device="cpu" if on_host else acc.device)
+        now = time.perf_counter()
+        el = torch.tensor([now - t0, now - t_start], dtype=torch.float64, device="cpu" if on_host else acc.device)
         dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
-        times[(ex, ch, sh)] = float(el.item()) / max(1, rounds) * 1e3
-    best = min(range(len(cands)), key=lambda i: (times[cands[i]], i))
+        times[(ex, ch, sh)] = float(el[0].item()) / max(1, rounds) * 1e3
+        if budget_s is not None and float(el[1].item()) > budget_s:
+            break
+    timed = [i for i in range(len(cands)) if cands[i] in times]
+    best = min(timed, key=lambda i: (times[cands[i]], i))
     return cands[best], times
 
 

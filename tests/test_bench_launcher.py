@@ -89,3 +89,77 @@ def test_external_launcher_is_respected():
     assert line["n_gpus"] == 2
     assert line["config"]["launched_by"] == "external launcher"
     assert line["config"]["workload"] == "fedavg_resnet18_fp32_256_clients_sharded_over_2_gpus"
+
+
+def _run_env(extra_env: dict, *args: str, timeout: float = 240.0) -> subprocess.CompletedProcess:
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env.update(extra_env)
+    return subprocess.run([sys.executable, str(REPO / "bench.py"), *args], cwd=REPO, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_hung_native_rank_is_named_and_the_launcher_reruns_with_torch_comm():
+    # rank 1 hangs in the timed stage only with the native communicator: its watchdog ends it
+    # (status 124, stage named), the launcher reports every rank's stage and starts ONE fresh set
+    # of ranks with --comm torch, whose line says it is the rerun
+    import time as _time
+
+    t0 = _time.monotonic()
+    r = _run_env({"BENCH_INJECT_HANG": "1:timed:native"}, "--gpus", "2", "--dry-run", "--steps", "2",
+                 "--stage-timeout", "5")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "rank 1: stage 'timed' still running after 5 s" in r.stderr
+    assert "rank 1 exited with status 124" in r.stderr and "last stage 'timed'" in r.stderr
+    assert "retrying once with fresh rank processes and --comm torch" in r.stderr
+    (line,) = _json_lines(r.stdout)
+    assert "--comm torch rerun" in line["config"]["launch_fallback"]
+    assert _time.monotonic() - t0 < 120
+
+
+def test_a_hang_in_both_runs_fails_within_the_budget():
+    import time as _time
+
+    t0 = _time.monotonic()
+    r = _run_env({"BENCH_INJECT_HANG": "1:timed:any"}, "--gpus", "2", "--dry-run", "--stage-timeout", "4",
+                 "--launch-timeout", "100")
+    assert r.returncode != 0 and _json_lines(r.stdout) == []
+    # rank 1 hangs, rank 0 waits for it in the timed stage's collective: both watchdogs fire, in the
+    # run and in its one rerun
+    assert r.stderr.count("rank 1: stage 'timed' still running") == 2
+    assert r.stderr.count("retrying once") == 1
+    assert _time.monotonic() - t0 < 100
+
+
+def test_launch_timeout_names_the_stage_of_every_rank():
+    # no watchdog (--stage-timeout 0): the launcher's own limit stops the run and says where each
+    # rank was
+    r = _run_env({"BENCH_INJECT_HANG": "0:shards:any"}, "--gpus", "2", "--dry-run", "--stage-timeout", "0",
+                 "--launch-timeout", "20", "--no-fallback")
+    assert r.returncode != 0
+    assert "ranks still running after --launch-timeout 20 s" in r.stderr
+    assert "rank 0 still running, last stage 'shards'" in r.stderr
+    assert "retrying" not in r.stderr
+
+
+def test_watchdog_fails_a_torchrun_job_fast():
+    # the driver's launcher form: the hung rank ends itself, torchrun stops the job
+    import time as _time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env["BENCH_INJECT_HANG"] = "1:timed:any"
+    sys.path.insert(0, str(REPO))
+    from bench import _free_port
+
+    t0 = _time.monotonic()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        str(REPO / "bench.py"), "--gpus", "2", "--dry-run", "--stage-timeout", "5"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0
+    # the hung rank or the one waiting for it in the stage's collective fires first; torchrun then
+    # stops the other
+    assert "stage 'timed' still running after 5 s" in r.stderr
+    assert _time.monotonic() - t0 < 120

@@ -399,6 +399,26 @@ def hbm_probes(device: torch.device, nbytes: int = 4 << 30) -> dict:
     return out
 
 
+def host_cpu() -> dict:
+    """The host the CPU baseline ran on (its rate moves several-fold between the pool's boxes: the
+    model, the CPUs this process may use, and the machine's total)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"model": model, "usable_cpus": usable, "machine_cpus": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dtype: torch.dtype = torch.float32) -> dict:
     """The reference's CPU path on the host cores, rank 0, N=1: the reference's
     FedAVGAlgorithm call sequence (oracle/ref_torch_cpu.py: process_worker_data per client with
@@ -434,6 +454,7 @@ def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dty
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
+        "host_cpu": host_cpu(),
         "seconds_per_round": round(best, 4),
         "sample": (
             f"the full round: {n_clients} pre-built ParameterMessages x {layout.num_segments}-tensor layout "
@@ -475,6 +496,7 @@ def cpu_baseline_personalized(layout: ModelLayout, budget_s: float = 12.0, worke
         "folds_per_s": round(workers * (workers - 1) * layout.total_numel / best, 1),
         "cores": threads,
         "kind": "port",
+        "host_cpu": host_cpu(),
         "sample": (
             f"{workers} workers x {workers} receivers x ResNet-18 layout fp32, reference op sequence "
             "(deepcopy per receiver, isnan, to(f64)*w, +=, /W, isnan; centralized weighted_avg) in torch CPU, "
@@ -651,6 +673,7 @@ def cpu_baseline_qsgd(layout: ModelLayout, budget_s: float = 12.0, sample_client
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
+        "host_cpu": host_cpu(),
         "sample": (
             f"{sample_clients} QSGD-quantised clients x ResNet-18 layout (fp32 codec, level 255): host "
             f"dequantisation (unpack signs, norm * sign * slot / level) + the reference FedAvg op sequence "
@@ -696,6 +719,7 @@ def cpu_baseline_nnadq(layout: ModelLayout, budget_s: float = 12.0, sample_clien
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
+        "host_cpu": host_cpu(),
         "sample": (
             f"{sample_clients} NNADQ-quantised clients x ResNet-18 layout (fp32 codec): host dequantisation "
             f"(code * step + lo) + the reference FedAvg op sequence in torch CPU, best of {len(times)} runs "
@@ -901,6 +925,138 @@ def main_plugin(args: argparse.Namespace) -> int:
             "kernel": f"fedavg_tile_kernel x {n_waves} launch(es) per round", "bytes_per_step": launch_bytes,
             "kernel_ms_per_step": round(kstep_s * 1e3, 4), "launches": launches},
         "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def main_multi(args: argparse.Namespace) -> int:
+    """--procs 1 --gpus N: ONE process drives N GPUs through the single-process multi-device mode
+    (include/fedavg_hip.h fedavg_multi_*) — the structure of the reference's single
+    server process (simulation_lib/server/server.py:122-152). BASELINE config 3 (256 clients,
+    contiguous shards), the peer-window exchange (or --multi-exchange reduce: in-process RCCL); the
+    (exchange, chunks, shape) candidate is timed on the node before the warmup (--tune-budget),
+    or taken from the cost model with --no-tune. --alias: every entry on cuda:0 (a one-GPU code-path
+    rehearsal, not an N-GPU measurement)."""
+    from distributed_learning_simulation_lib_amd.multi_device import MultiDeviceContext
+
+    G = args.gpus
+    devices = [0] * G if args.alias else list(range(G))
+    if not args.alias and torch.cuda.device_count() < G:
+        raise SystemExit(f"--procs 1 --gpus {G}: only {torch.cuda.device_count()} GPU(s) visible (--alias rehearses)")
+    in_dtype, out_dtype = getattr(torch, args.in_dtype), getattr(torch, args.out_dtype)
+    layout = LAYOUTS[args.layout]()
+    P, T = layout.total_numel, layout.num_segments
+    n_total = job_clients(args, G)
+    weights_all = dataset_size_weights(n_total)
+    m = MultiDeviceContext(layout, devices)
+    keep, tables = [], []
+    for g, d in enumerate(devices):
+        lo, hi = shard_bounds(n_total, G, g)
+        dev = torch.device("cuda", d)
+        buckets, views = make_clients(layout, lo, hi - lo, dev, in_dtype)
+        keep.append(buckets)
+        t = ClientTable(T)
+        for row, w in zip(views, weights_all[lo:hi]):
+            t.add_client(row, [w] * T)
+        tables.append(t if hi > lo else None)
+    partials = m.plan_partials(tables, in_dtype)
+    root_dev = torch.device("cuda", devices[0])
+    offs, padded = layout.padded_offsets(out_dtype.itemsize)
+    out_flat = torch.empty(padded, dtype=out_dtype, device=root_dev)
+    outs = OutputTable([out_flat[o : o + n] for o, n in zip(offs, layout.numels)], layout, root_dev, out_dtype)
+    totals = [float(sum(weights_all))] * T
+    nt = m.num_tiles
+    model = ExchangeModel()
+    in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
+    exchanges = (args.multi_exchange,)
+    cands = exchange_candidates(args.chunks or None, exchanges=exchanges)
+
+    def sync_all() -> None:
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    def one_round(ex: str, edges: list[int]) -> None:
+        m.round(partials, totals, outs, out_dtype, root=0, edges=edges, exchange=ex)
+        m.raise_on_nan([[(t, in_dtype)] if t is not None else [] for t in tables])
+
+    tuned, selection = None, "cost model"
+    if args.no_tune:
+        (ex, ch, sh), _ = model.best(G, P, n_total, in_b, out_b, nt, cands, balance_root=False)
+    else:
+        times, t_start = {}, time.perf_counter()
+        for cand in cands:
+            e = chunk_edges(nt, cand[1], cand[2])
+            one_round(cand[0], e)
+            sync_all()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                one_round(cand[0], e)
+            sync_all()
+            times[cand] = (time.perf_counter() - t0) / 3 * 1e3
+            if time.perf_counter() - t_start > args.tune_budget:
+                break
+        ex, ch, sh = min(times, key=lambda c: (times[c], cands.index(c)))
+        tuned = {f"{a}/{b}/{c}": round(v, 4) for (a, b, c), v in times.items()}
+        selection = "tuned"
+    edges = chunk_edges(nt, ch, sh)
+    for _ in range(args.warmup):
+        one_round(ex, edges)
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_round(ex, edges)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    step_s = elapsed / args.steps
+    job_bytes = n_total * P * in_b + P * out_b
+    value = job_bytes / step_s / 1e9
+
+    # the dominant kernel, after the timed region: entry 0's windowed partial launches (one per
+    # chunk) timed with HIP events on its stream over the same number of rounds
+    ctx0 = m.contexts[0]
+    ctx0.prof_collect()
+    ctx0.prof_enable(not args.no_kernel_events)
+    for _ in range(args.steps):
+        one_round(ex, edges)
+    sync_all()
+    ctx0.prof_enable(False)
+    kernel_ms, launches = ctx0.prof_collect()
+    lo0, hi0 = shard_bounds(n_total, G, 0)
+    rank_bytes = P * (hi0 - lo0) * in_b + P * 8  # its clients' reads + its fp64 partial stores (local or peer)
+    kernel_step_ms = kernel_ms / args.steps
+    achieved = rank_bytes / (kernel_step_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    predicted = model.round_ms(G, P, n_total, in_b, out_b, edges, ex) if G > 1 else None
+    one_gpu = model.one_gpu_ms(P, n_total, in_b, out_b)
+    m.close()
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": len(set(devices)), "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
+        "config": {
+            "workload": workload_name(args, G, n_total, 1, n_total // G) + "_one_process",
+            "total_clients": n_total, "device_entries": devices, "params_per_client": P, "tensors_per_client": T,
+            "in_dtype": args.in_dtype, "accumulate_dtype": "float64", "out_dtype": args.out_dtype,
+            "parallelism": f"one process, {G} device entries: clients sharded, "
+                           + ("peer-window exchange over xGMI (fedavg_multi_round)" if ex == "peer"
+                              else "in-process RCCL reduce (fedavg_multi_round)"),
+            "exchange": {"mode": ex, "chunks": ch, "chunk_shape": sh, "selection": selection,
+                         "tuned_ms_per_round": tuned,
+                         "predicted_speedup": None if predicted is None else predicted["speedup"],
+                         "predicted": predicted, "one_gpu_model_ms": round(one_gpu, 4)},
+            "baseline_config": "BASELINE.json configs[2] driven from one process" if n_total == 256 else "see DESIGN.md",
+            **({"rehearsal": f"all {G} entries on cuda:0: a code-path check of the exchange, not an N-GPU measurement"}
+               if args.alias else {}),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": f"fedavg_tile_kernel<{args.in_dtype}, OUT_ACC, windowed> on entry 0 (its chunk launches)",
+            "bytes_per_step_this_rank": rank_bytes, "kernel_ms_per_step": round(kernel_step_ms, 4),
+            "launches": launches,
+        },
+        "cpu_baseline": None,
     }
     print(json.dumps(line), flush=True)
     return 0
@@ -1177,6 +1333,8 @@ def main() -> int:
     ap.add_argument("--procs", type=int, default=0,
                     help="--procs 1 with --gpus N: one process drives the N GPUs (fedavg_multi_*, the "
                          "single-process multi-device mode) instead of one rank process per GPU")
+    ap.add_argument("--alias", action="store_true",
+                    help="--procs 1: every device entry on cuda:0 (a one-GPU rehearsal of the multi-device round)")
     ap.add_argument("--multi-exchange", default="peer", choices=["peer", "reduce"],
                     help="--procs 1: the peer-window exchange (no collective library) or the in-process RCCL reduce")
     ap.add_argument("--dry-run", action="store_true",
@@ -1198,6 +1356,8 @@ def main() -> int:
         return main_plugin(args)
     if args.shard == "elements":
         return main_elements(args)
+    if args.procs == 1 and args.gpus > 1:
+        return main_multi(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

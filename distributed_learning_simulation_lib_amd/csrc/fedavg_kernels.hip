@@ -67,13 +67,10 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 // scripts/tune_kernel.py, see DESIGN.md "Kernel tuning"):
 //   FEDAVG_AE        elements owned by one lane (= fp64 accumulators per lane)
 //   FEDAVG_CU_BYTES  bytes of client loads in flight per lane per group
-//   FEDAVG_NT        1 = non-temporal (streaming) client loads
-//   FEDAVG_LOAD_FENCE 1 = sched_barrier between a group's loads and its folds
-//   FEDAVG_NT_STORE  1 = non-temporal result / accumulator stores
-// Measured on MI355X (64 x ResNet-18 fp32 -> fp32, interleaved A/B in one process):
-// nt loads ~+1-2 %, nt stores +5-9 % (a read stream with interleaved writes loses HBM
-// efficiency; nt stores cut that), AE 16 / CU 512 B +-1 %, load fence / 128-512-thread
-// groups / fused fold within noise. Shipped: AE 8, CU 256 B, nt loads and stores.
+// Client loads and result stores are non-temporal (measured on MI355X, 64 x ResNet-18 fp32 ->
+// fp32, interleaved A/B in one process: nt loads ~+1-2 %, nt stores +5-9 % — a read stream with
+// interleaved writes loses HBM efficiency; nt stores cut that); AE 16 / CU 512 B +-1 %, load
+// fence / 128-512-thread groups / fused fold within noise.
 #ifndef FEDAVG_AE
 #define FEDAVG_AE 16
 #endif
@@ -98,24 +95,6 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 // 0.974-0.984 ms; AE 8 / 768 B, AE 4, AE 32 and AE 16 / 512 B no better than the old default)
 #define FEDAVG_CU_BYTES_F64 512
 #endif
-#ifndef FEDAVG_NT
-#define FEDAVG_NT 1
-#endif
-#ifndef FEDAVG_LOAD_FENCE
-#define FEDAVG_LOAD_FENCE 0
-#endif
-#ifndef FEDAVG_MIN_WAVES  // __launch_bounds__ minimum waves per SIMD (caps VGPRs: 8 -> <= 64)
-#define FEDAVG_MIN_WAVES 1
-#endif
-#ifndef FEDAVG_PERSISTENT  // exact-order kernel as a persistent grid (resident blocks x CUs)
-#define FEDAVG_PERSISTENT 0
-#endif
-#ifndef FEDAVG_ABLATE_EPILOGUE
-#define FEDAVG_ABLATE_EPILOGUE 0
-#endif
-#ifndef FEDAVG_NT_STORE
-#define FEDAVG_NT_STORE 1
-#endif
 // Software-pipelined client loads (the next stage's loads issue before the current stage folds),
 // one bit per input size: 1 = 2-byte, 2 = 4-byte, 4 = 8-byte. Interleaved A/B on MI355X
 // (scripts/tune_kernel.py, 64-byte stages = 4 fp16 / bf16 clients): 64 x ResNet-18 fp16
@@ -130,17 +109,8 @@ constexpr int kThreads = 256;     // 4 waves of 64 (split kernel, probes)
 // same for fp32 (all stores plain) cost ViT-B/16 waves 2.4 % (kept non-temporal there)
 #define FEDAVG_ACC_PLAIN_STORE_HALF 1
 #endif
-#ifndef FEDAVG_ACC_PLAIN_STORE_F32  // the same for fp32 / fp64 inputs (A/B knobs)
-#define FEDAVG_ACC_PLAIN_STORE_F32 0
-#endif
-#ifndef FEDAVG_ACC_PLAIN_STORE_F64
-#define FEDAVG_ACC_PLAIN_STORE_F64 0
-#endif
 #ifndef FEDAVG_BALANCE_DEFAULT  // balanced whole-layout tile orders (bit 0 fp32, bit 1 fp64); env FEDAVG_BALANCE
 #define FEDAVG_BALANCE_DEFAULT 3
-#endif
-#ifndef FEDAVG_ACC_NT_LOAD  // 1 = the continuing accumulator is read with non-temporal loads
-#define FEDAVG_ACC_NT_LOAD 0
 #endif
 #ifndef FEDAVG_WALK_ALTERNATE  // streaming waves alternate their tile walk (env FEDAVG_WALK_ALTERNATE)
 #define FEDAVG_WALK_ALTERNATE 1
@@ -154,12 +124,6 @@ constexpr int kTile1 = FEDAVG_TILE1;          // 4096 elements, SPLIT = 1 (any d
 #define FEDAVG_TILE_WIDE 8192
 #endif
 constexpr int kTileWide = FEDAVG_TILE_WIDE;
-#ifndef FEDAVG_F64_WIDE  // 1 = fp64 whole-layout launches use the wide table too (A/B knob)
-#define FEDAVG_F64_WIDE 0
-#endif
-#ifndef FEDAVG_AE_F64_WIDE  // elements per lane for fp64 inputs on wide tiles
-#define FEDAVG_AE_F64_WIDE 16
-#endif
 constexpr int kTile4 = (kThreads / 4) * kAE;  // 1024 elements, SPLIT = 4
 
 struct TileDesc {
@@ -192,12 +156,18 @@ struct KArgs {
   double* acc;
   uint32_t* flag;
   int32_t tile_begin;
-  int32_t num_tiles;   // tiles of this launch (persistent grid-stride bound)
+  int32_t num_tiles;   // tiles of this launch
   int32_t K;           // row stride of the [T][K] tables
   int32_t zero_init;   // start every segment at the identity -0.0, ignore acc_in (shard partials)
   int32_t walk_back;   // the first walk_back tiles of the launch are walked last to first
                        // (fedavg_ctx::walk_reverse); 0 = natural order
   const double* qtab;  // QSGD: [T][K][256] |product| tables of the call (qsgd_table_kernel)
+  // Multi-device peer exchange (multi_device.cpp): a zero-initialised partial launch whose tiles
+  // [win_edge[j], win_edge[j+1]) store into win_dst[j] (device j's receive slot for this device,
+  // accumulator coordinates) instead of acc; win_n = G windows, NULL = not windowed.
+  double* const* win_dst;
+  const int32_t* win_edge;
+  int32_t win_n;
 };
 
 enum OutKind : int { OUT_ACC = 0, OUT_F32 = 1, OUT_F64 = 2 };
@@ -357,11 +327,7 @@ struct LaneLoader {
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       if (FULL || v < nv) {
-#if FEDAVG_NT
         buf[v] = __builtin_nontemporal_load(vb + v * LANES + li);
-#else
-        buf[v] = vb[v * LANES + li];
-#endif
       } else {
         buf[v] = V{};
       }
@@ -403,7 +369,7 @@ template <typename T, int SPLIT, int TILEN = kTile1>
 struct Geo {
   static constexpr int AE = (SPLIT > 1) ? kAE
                           : (sizeof(T) == 2 ? FEDAVG_AE_HALF
-                             : sizeof(T) == 8 ? (TILEN == kTile1 ? FEDAVG_AE_F64 : FEDAVG_AE_F64_WIDE)
+                             : sizeof(T) == 8 ? FEDAVG_AE_F64
                                               : kAE);
   static constexpr int LANES = (SPLIT > 1) ? 64 : TILEN / AE;
   static constexpr int THREADS = (SPLIT > 1) ? kThreads : LANES;
@@ -420,14 +386,10 @@ __device__ __forceinline__ void raise_flag(uint32_t* flag, int word) {
   __hip_atomic_store(flag + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Vector store of a result/accumulator slice (non-temporal when FEDAVG_NT_STORE).
+// Non-temporal vector store of a result / accumulator slice.
 template <typename V>
 __device__ __forceinline__ void store_out(gptr<V> p, V v) {
-#if FEDAVG_NT_STORE
   __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
 }
 
 // One fp64 fold step. The reference rounds the product and the sum separately
@@ -508,11 +470,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
       for (int j = 0; j < N; j += 2) {
         if (FULL || e + j + 2 <= count) {
-#if FEDAVG_ACC_NT_LOAD
-          const f64x2 d = __builtin_nontemporal_load((gptr<const f64x2>)(ap + e + j));
-#else
-          const f64x2 d = *(gptr<const f64x2>)(ap + e + j);
-#endif
+          const f64x2 d = *(gptr<const f64x2>)(ap + e + j);  // plain: non-temporal measured -14 %
           acc[v * N + j] = d.x;
           acc[v * N + j + 1] = d.y;
         } else {
@@ -625,9 +583,6 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
         wk[c] = wp[kc];
         LL::load_raw(client(kc), li, buf[c], nv);
       }
-#if FEDAVG_LOAD_FENCE
-      __builtin_amdgcn_sched_barrier(0);  // every load of the group issues before any fold
-#endif
 #pragma unroll
       for (int c = 0; c < CU_LOADS; ++c) {
 #pragma unroll
@@ -697,7 +652,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const bool in_range = FULL || (e + j < count);
-      bad_acc |= in_range && (acc[v * N + j] != acc[v * N + j]) && !FEDAVG_ABLATE_EPILOGUE;
+      bad_acc |= in_range && (acc[v * N + j] != acc[v * N + j]);
     }
   }
 
@@ -710,8 +665,8 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
       for (int j = 0; j < N; j += 2) {
         if (FULL || e + j + 2 <= count) {
           const f64x2 pair = f64x2{acc[v * N + j], acc[v * N + j + 1]};
-          if constexpr ((sizeof(T) == 2 && FEDAVG_ACC_PLAIN_STORE_HALF) ||
-                        (sizeof(T) == 4 && FEDAVG_ACC_PLAIN_STORE_F32) || (sizeof(T) == 8 && FEDAVG_ACC_PLAIN_STORE_F64)) {
+          // (plain stores for fp32 / fp64 waves too measured -1.3 ... -3.7 %: kept non-temporal)
+          if constexpr (sizeof(T) == 2 && FEDAVG_ACC_PLAIN_STORE_HALF) {
             *(gptr<f64x2>)(ap + e + j) = pair;  // see FEDAVG_ACC_PLAIN_STORE_HALF
           } else {
             store_out((gptr<f64x2>)(ap + e + j), pair);
@@ -728,19 +683,14 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
     const double W = to_const<double>(a.tab.wtot)[seg];
     bool bad_res = false;
     double res[AE];
-#if FEDAVG_ABLATE_EPILOGUE  // timing-only build: reciprocal multiply, no NaN checks (wrong results)
-#pragma unroll
-    for (int i = 0; i < AE; ++i) res[i] = acc[i] * (1.0 / W);
-#else
     exact_div_block<AE>(acc, res, W);
-#endif
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int e = (v * LANES + li) * N;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         const bool in_range = FULL || (e + j < count);
-        bad_res |= in_range && (res[v * N + j] != res[v * N + j]) && !FEDAVG_ABLATE_EPILOGUE;
+        bad_res |= in_range && (res[v * N + j] != res[v * N + j]);
       }
     }
     void* const out_raw = reinterpret_cast<void*>(to_const<uint64_t>(a.tab.outs)[seg]);
@@ -802,14 +752,30 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 // instantiation: compiled into every launch, that path cost the plain whole-layout launch 3-4 %
 // (VGPRs 131 -> 144, twice the code; profiles/r03_ab_matrix.txt).
 template <typename T, int OUT, int SPLIT, bool VEC, int FOLD, int TILEN = kTile1, bool PV = false>
-__global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) void fedavg_tile_kernel(KArgs a) {
+__global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS)) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
   constexpr int TILE = Geo<T, SPLIT, TILEN>::TILE;
-  // Persistent form (exact-order kernel): a grid of (resident blocks) workgroups walks the
-  // tiles with stride gridDim.x, so the tiles in flight at any moment are one contiguous range
-  // of every client bucket and no block is launched per tile. The split kernel keeps one
-  // tile per workgroup (its LDS combine ends with the non-zero waves leaving).
+  // One workgroup per tile (a persistent grid walking the tiles measured 2 % slower and is not
+  // kept). The split kernel's LDS combine ends with the non-zero waves leaving.
   const int ntiles = (SPLIT == 1) ? a.num_tiles : static_cast<int>(gridDim.x);
+  if constexpr (OUT == OUT_ACC && SPLIT == 1) {
+    if (a.win_dst != nullptr) {
+      // windowed partial (multi-device peer exchange): the tile's window picks the destination,
+      // a wave-uniform scan of at most FEDAVG_MULTI_MAX_DEVICES scalar edges
+      for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int32_t ti = a.tile_begin + t;
+        const kptr<int32_t> we = to_const<int32_t>(a.win_edge);
+        int j = 0;
+        while (j + 1 < a.win_n && ti >= we[j + 1]) ++j;
+        KArgs b = a;
+        b.acc = reinterpret_cast<double*>(to_const<uint64_t>(a.win_dst)[j]);
+        const TileDesc td = load_tile(a.tiles, ti);
+        if (td.count == TILE) tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN>(b, td, lds);
+        else tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN>(b, td, lds);
+      }
+      return;
+    }
+  }
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const TileDesc td = load_tile(a.tiles, a.tile_begin + (t < a.walk_back ? a.walk_back - 1 - t : t));
     constexpr int LV = Geo<T, SPLIT, TILEN>::LANES * Vec16<T>::n;  // elements per lane-vector row
@@ -856,57 +822,19 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS), FEDAVG_MIN_WAVES) 
 // [16 li, 16 li + 16) (one 16-B slot load + one 2-B sign load per client; a wave reads 1 KiB of
 // slots contiguously). Clients go in groups of QG: the group's loads are issued, its QG tables
 // are built into one of two LDS buffers, one barrier, then the fold in arrival order.
-#ifndef FEDAVG_QSGD_PIPE  // 1: a client's table reads issued under the previous client's adds
-#define FEDAVG_QSGD_PIPE 0
-#endif
-#ifndef FEDAVG_QSGD_READ_FENCE
-#define FEDAVG_QSGD_READ_FENCE 1
-#endif
-#ifndef FEDAVG_QSGD_ABLATE
-#define FEDAVG_QSGD_ABLATE 0
-#endif
-#ifndef FEDAVG_QSGD_AE
-#define FEDAVG_QSGD_AE 16  // elements per lane: 16 (256-lane workgroups) or 8 (512 lanes)
-#endif
-static_assert(FEDAVG_QSGD_AE == 16 || FEDAVG_QSGD_AE == 8, "QSGD lanes hold 16 or 8 elements");
-// one wave of the workgroup DMAs each client table of a group: clients per group = waves
-#ifndef FEDAVG_QSGD_GROUP  // clients per group, at most one per wave (2: 82 VGPRs, 5 waves/SIMD)
-#define FEDAVG_QSGD_GROUP 2
-#endif
+// The built geometry (wider tiles, 512-entry signed tables, deeper prefetch, one-wave
+// workgroups, a pipelined fold and packed loads were measured no faster and are not kept).
+constexpr int kQsgdAE = 16;       // elements per lane (256-lane workgroups on 4096-element tiles)
+constexpr int kQsgdGroup = 2;     // clients per group (82 VGPRs, 5 waves per SIMD)
 #ifndef FEDAVG_QSGD_RB  // table reads per batch before their adds (elements of a lane)
 #define FEDAVG_QSGD_RB 4
 #endif
-static_assert(FEDAVG_QSGD_GROUP >= 1 && FEDAVG_QSGD_GROUP <= 4096 / FEDAVG_QSGD_AE / 64, "one table DMA per wave");
-constexpr int kQsgdGroup = FEDAVG_QSGD_GROUP;
-#ifndef FEDAVG_QSGD_DEPTH
-#define FEDAVG_QSGD_DEPTH 1
-#endif
-// groups whose loads are in flight while a group folds; DEPTH + 1 LDS table buffers
-constexpr int kQsgdDepth = FEDAVG_QSGD_DEPTH;
-constexpr int kQsgdBufs = kQsgdDepth + 1;
-static_assert(kQsgdDepth >= 1 && kQsgdDepth <= 3, "QSGD prefetch depth 1..3");
-
-#ifndef FEDAVG_QSGD_SIGNED  // 1: 512-entry signed tables indexed by (non-negative << 8 | slot)
-#define FEDAVG_QSGD_SIGNED 0
-#endif
-constexpr int kQsgdSlots = 256;  // slot values
-// table entries per client: |p| per slot value, or (signed form) -p | +p per slot value
-constexpr int kQsgdTable = FEDAVG_QSGD_SIGNED ? 512 : 256;
-#ifndef FEDAVG_QSGD_WPE  // > 0: ask the compiler for at least this many waves per SIMD
-#define FEDAVG_QSGD_WPE 0
-#endif
-#ifndef FEDAVG_QSGD_WIDE  // 1: whole-layout launches fold 8192-element tiles (512 lanes)
-#define FEDAVG_QSGD_WIDE 0
-#endif
-#ifndef FEDAVG_QSGD_DMA_SPLIT  // 1: a group's table chunks split over the waves (no duplicate DMAs)
-#define FEDAVG_QSGD_DMA_SPLIT 1
-#endif
-#ifndef FEDAVG_QSGD_SOLO  // 1: one-wave workgroups (a quarter tile each) that DMA their own tables
-#define FEDAVG_QSGD_SOLO 0
-#endif
-constexpr int kQsgdAE = FEDAVG_QSGD_AE;
+constexpr int kQsgdSlots = 256;   // slot values
+constexpr int kQsgdTable = 256;   // |p| per slot value
+constexpr int kQsgdBufs = 2;      // LDS table buffers: the next group's DMAs land while a group folds
 constexpr int kQsgdTileLanes = 4096 / kQsgdAE;  // lanes covering one 4096-element tile
-constexpr int kQsgdLanes = FEDAVG_QSGD_SOLO ? 64 : kQsgdTileLanes;  // lanes per workgroup
+constexpr int kQsgdLanes = kQsgdTileLanes;       // lanes per workgroup (one tile each)
+static_assert(kQsgdGroup * kQsgdTable / 128 == kQsgdLanes / 64, "one 1-KiB table DMA chunk per wave and group");
 
 template <typename DQ>
 __device__ __forceinline__ double qsgd_product(double norm, int level, int slot, double w) {
@@ -936,15 +864,6 @@ __global__ __launch_bounds__(kQsgdSlots) void qsgd_table_kernel(CallTables tab, 
   const int level = to_const<int32_t>(rec)[2];
   const double w = to_const<double>(tab.w)[row];
   const int s = static_cast<int>(threadIdx.x);
-#if FEDAVG_QSGD_SIGNED
-  // entry 256 + s: the product of a non-negative element of slot s (sign(norm) * sign(w)),
-  // entry s: its negation, the product of a negative element (every step is sign-symmetric,
-  // zeros included), so the fold indexes the table with (sign bit << 8 | slot) and adds
-  const double pp = qsgd_product<DQ>(norm, level, s, w);
-  qtab[row * kQsgdTable + kQsgdSlots + s] = pp;
-  qtab[row * kQsgdTable + s] = -pp;
-  return;
-#endif
   const double p = __builtin_fabs(qsgd_product<DQ>(norm, level, s, w));
   // entry 0 is a zero (or a NaN, for a non-finite norm / weight): its sign bit carries the
   // client's product sign, signbit(norm) ^ signbit(w), which the fold reads with one broadcast
@@ -1064,16 +983,14 @@ __device__ __forceinline__ void qsgd_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int OUT, typename DQ, bool FULL, bool VEC, int TILEN = 4096>
-__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable],
-                                               int lane_base) {
+template <int OUT, typename DQ, bool FULL, bool VEC>
+__device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& td, double (*lut)[kQsgdGroup][kQsgdTable]) {
   constexpr int AE = kQsgdAE;
   constexpr int G = kQsgdGroup;
-  constexpr int D = kQsgdDepth;
   constexpr int NB = kQsgdBufs;
   const int seg = td.seg;
   const int count = td.count;
-  const int li = lane_base + static_cast<int>(threadIdx.x);
+  const int li = static_cast<int>(threadIdx.x);
   const int e0 = li * AE;  // first element of this lane within the tile
   const bool lane_live = FULL || e0 < count;
 
@@ -1090,30 +1007,14 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   double acc[AE];
   bool have = record_tile_acc_in<FULL, AE>(a, seg, acc_base, e0, count, acc);
 
-  // Client loads of one group (slots + sign words) and its G |product| tables (global -> LDS
-  // by DMA: wave w moves client k + w's 2 KiB table in two 1-KiB global_load_lds_dwordx4, the
-  // last client again for a short group), issued D groups ahead of the group's fold into one of
-  // D + 1 LDS buffers: every wave issues exactly kOps vector memory operations per group, so
-  // "the group D - 1 issues back has landed" is a counted vmcnt.
-  // DMA chunks of 1 KiB per wave and group: a 2-KiB table per client over the group's waves
-  // (waves past the group's size repeat the last table), or the 4-KiB signed tables spread
-  // evenly over the waves
-  constexpr int kWaves = (FEDAVG_QSGD_SOLO ? kQsgdLanes : TILEN / AE) / 64;
-  constexpr int kChunks = G * kQsgdTable / 128;  // 1-KiB DMA chunks of a group's tables
-  // more waves than chunks (8192-element tiles): waves past the chunks move nothing — their
-  // operation count differs, which only the one-group-ahead schedule (vmcnt(0) waits) allows
-  constexpr bool kSparse = !FEDAVG_QSGD_SOLO && kChunks < kWaves && FEDAVG_QSGD_DMA_SPLIT;
-  static_assert(!kSparse || kQsgdDepth == 1, "uneven DMA counts need the vmcnt(0) schedule");
-  // the chunks split evenly over the waves (no wave moves a table twice), or — when they do not
-  // — wave w moves client min(w, G - 1)'s whole table (waves past the group repeat the last one)
-  constexpr bool kSplit = FEDAVG_QSGD_SOLO || (FEDAVG_QSGD_DMA_SPLIT && kChunks % kWaves == 0);
-  constexpr int kDmaPerWave = kSplit ? kChunks / kWaves : kSparse ? 1 : 2;
-  static_assert(!FEDAVG_QSGD_SIGNED || kSplit, "signed tables split evenly over the waves");
-  constexpr int kOps = 2 * G + kDmaPerWave;
-  using SlotVec = typename std::conditional<AE == 16, u32x4, u32x2>::type;  // AE slot bytes
+  // Client loads of one group (slots + sign words) and its G |product| tables (global -> LDS by
+  // DMA: the group's 2-KiB tables are four 1-KiB chunks, wave w moves chunk w — the last table
+  // again for a short group), issued one group ahead of the group's fold into the other of two
+  // LDS buffers: every wave issues the same 2 G + 1 vector memory operations per group (a wave
+  // retires a group with vmcnt(0) before issuing the next one).
   struct GroupRegs {
-    SlotVec slots[G];
-    uint32_t signs[G];  // AE sign bits (16-bit / 8-bit load)
+    u32x4 slots[G];     // AE slot bytes
+    uint32_t signs[G];  // AE sign bits (16-bit load)
   };
   const int wave = __builtin_amdgcn_readfirstlane(li >> 6);
   const int lane = li & 63;
@@ -1128,46 +1029,16 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
       // (its loop-carried tracking otherwise drains vmcnt to 0 between groups); the counted wait
       // at the top of each step covers every use, and no register of a pending load is reused
       // before that use (the value is live from here to the fold)
-      if constexpr (AE == 16) {
-        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r.slots[c]) : "v"(rp + slot_off) : "memory");
-        asm volatile("global_load_ushort %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
-      } else {
-        asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(r.slots[c]) : "v"(rp + slot_off) : "memory");
-        asm volatile("global_load_ubyte %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
-      }
+      asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r.slots[c]) : "v"(rp + slot_off) : "memory");
+      asm volatile("global_load_ushort %0, %1, off" : "=v"(r.signs[c]) : "v"(rp + sign_off) : "memory");
     }
-    if constexpr (kSparse) {
-      if (wave < kChunks) {  // wave-uniform
-        const int cl = wave / (kQsgdTable / 128);
-        const int part = wave % (kQsgdTable / 128);
-        const double* src = tabs + static_cast<int64_t>(k + min(cl, n - 1)) * kQsgdTable + part * 128;
-        double* dst = lut[buf][cl] + part * 128;
-        __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
-                                         (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-      }
-    } else if constexpr (kSplit) {
-#pragma unroll
-    for (int q = 0; q < kDmaPerWave; ++q) {
-      // 1-KiB chunk of the group's tables (a one-wave workgroup moves all of them)
-      const int chunk = (FEDAVG_QSGD_SOLO ? 0 : wave * kDmaPerWave) + q;
-      const int cl = chunk / (kQsgdTable / 128);    // client of the group
-      const int part = chunk % (kQsgdTable / 128);  // 128 doubles each
-      const double* src = tabs + static_cast<int64_t>(k + min(cl, n - 1)) * kQsgdTable + part * 128;
-      double* dst = lut[buf][cl] + part * 128;
-      __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
-                                       (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-    }
-    } else {
-    // waves past the group's size move the group's last table again, into its own slot (the
-    // same bytes twice: every wave issues the same DMAs, so the counted wait holds)
-    const int tw = min(wave, G - 1);
-    const double* src = tabs + static_cast<int64_t>(k + min(tw, n - 1)) * kQsgdTable;
-    double* dst = lut[buf][tw];
+    // this wave's 1-KiB chunk of the group's tables
+    const int cl = wave / (kQsgdTable / 128);    // client of the group
+    const int part = wave % (kQsgdTable / 128);  // 128 doubles each
+    const double* src = tabs + static_cast<int64_t>(k + min(cl, n - 1)) * kQsgdTable + part * 128;
+    double* dst = lut[buf][cl] + part * 128;
     __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 2 * lane),
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((void FEDAVG_AS_GLOBAL*)(src + 128 + 2 * lane),
-                                     (void __attribute__((address_space(3)))*)(dst + 128), 16, 0, 0);
-    }
   };
   // Fold of one group from LDS buffer B (compile-time, so every table read is
   // `ds_read_b64 v, v_off offset:<buffer base>`). The table holds |p|; the sign of each
@@ -1178,79 +1049,6 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   auto run = [&](auto buf_tag, const GroupRegs& r, int k) {
     constexpr int B = decltype(buf_tag)::value;
     const int n = min(G, kseg - k);  // wave-uniform
-#if FEDAVG_QSGD_PIPE
-    // client c + 1's table reads in flight while client c's products are added (two register
-    // sets of AE doubles)
-    double pv[2][AE];
-    int32_t t0[2];
-    auto reads = [&](int c, double (&pa)[AE], int32_t& t) {
-      const char* tab = reinterpret_cast<const char*>(lut[B][c]);
-      t = reinterpret_cast<const int32_t*>(tab)[1];
-#pragma unroll
-      for (int j = 0; j < AE; ++j) {
-        const uint32_t word = r.slots[c][j >> 2];
-        const uint32_t off = ((word >> (8 * (j & 3))) & 0xffu) << 3;
-        pa[j] = *reinterpret_cast<const double*>(tab + off);
-      }
-    };
-    if (n > 0) reads(0, pv[0], t0[0]);
-#pragma unroll
-    for (int c = 0; c < G; ++c) {
-      if (c < n) {
-        if (c + 1 < n) reads(c + 1, pv[(c + 1) & 1], t0[(c + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t neg = r.signs[c] ^ ~static_cast<uint32_t>(t0[c & 1] >> 31);
-#pragma unroll
-        for (int j = 0; j < AE; ++j) {
-          const int bit = (j < 8) ? (7 - j) : (15 - (j - 8));
-          const uint32_t sb = neg << (31 - bit);
-          const uint64_t u = static_cast<uint64_t>(__double_as_longlong(pv[c & 1][j]));
-          const uint32_t hi = (sb & 0x80000000u) | (static_cast<uint32_t>(u >> 32) & 0x7fffffffu);
-          const double p = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (u & 0xffffffffull)));
-          acc[j] = acc[j] + p;
-        }
-      }
-    }
-    return;
-#endif
-#if FEDAVG_QSGD_SIGNED
-    static_assert(AE == 16, "the signed fold spreads a 16-bit sign word");
-#pragma unroll
-    for (int c = 0; c < G; ++c) {
-      if (c < n) {
-        const char* tab = reinterpret_cast<const char*>(lut[B][c]);
-        // numpy.packbits order puts element j < 8 at bit 7 - j and j >= 8 at bit 23 - j of the
-        // 16-bit word (1 = non-negative); reversed, element j sits at bit 24 + j (j < 8) or
-        // 8 + j (j >= 8): four consecutive elements are one nibble
-        const uint32_t rev = __builtin_bitreverse32(r.signs[c]);
-#pragma unroll
-        for (int q = 0; q < AE / 4; ++q) {  // elements 4q .. 4q + 3: slot word q
-          const int pos = (q < 2) ? 24 + 4 * q : 8 + 4 * q;
-          // nibble -> one byte per element (bit i -> bit 8 i), each 0 or 1
-          const uint32_t sb4 = (((rev >> pos) & 0xfu) * 0x00204081u) & 0x01010101u;
-          const uint32_t word = r.slots[c][q];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {  // elements 4q + 2h, 4q + 2h + 1
-            // two 16-bit table indices (sign << 8 | slot) in one v_perm_b32
-            const uint32_t sel = h ? 0x07030602u : 0x05010400u;
-            const uint32_t idx2 = __builtin_amdgcn_perm(sb4, word, sel);
-            // byte offsets: the low index by one SDWA shift of its word (the compiler emits a
-            // shift + mask), the high one as idx2 >> 13 (bits 13-15 of the low index are 0)
-            uint32_t off0;
-            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
-                : "=v"(off0) : "v"(3u), "v"(idx2));
-            const uint32_t off1 = idx2 >> 13;
-            double pv[2];
-            pv[0] = *reinterpret_cast<const double*>(tab + off0);
-            pv[1] = *reinterpret_cast<const double*>(tab + off1);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) acc[4 * q + 2 * h + e] = acc[4 * q + 2 * h + e] + pv[e];
-          }
-        }
-      }
-    }
-    return;
-#endif
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c < n) {
@@ -1269,15 +1067,11 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
             const int j = j0 + jj;
             const uint32_t word = r.slots[c][j >> 2];
             const uint32_t off = ((word >> (8 * (j & 3))) & 0xffu) << 3;
-#if FEDAVG_QSGD_ABLATE == 1  // timing only: no table reads (wrong results)
-            pav[jj] = static_cast<double>(off);
-#else
             pav[jj] = *reinterpret_cast<const double*>(tab + off);
-#endif
           }
-#if FEDAVG_QSGD_READ_FENCE
+          // the batch's reads are issued before its adds (the compiler would otherwise keep ~4
+          // outstanding and wait on each)
           __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
           for (int jj = 0; jj < RB; ++jj) {
             const int j = j0 + jj;
@@ -1294,14 +1088,12 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
       }
     }
   };
-  // Group i folds from buffer i % NB. At the top of each step a wave waits until its loads and
-  // DMAs of that group landed (the groups issued after it may stay in flight), and the barrier
-  // publishes every wave's DMAs; only then is group i + D issued, into buffer (i + D) % NB —
-  // the buffer of group i - 1, which the barrier proves every wave has finished reading.
+  // Group i folds from buffer i % 2. At the top of each step a wave waits until its loads and
+  // DMAs of that group landed, and the barrier publishes every wave's DMAs; only then is group
+  // i + 1 issued, into buffer (i + 1) % 2 — the buffer of group i - 1, which the barrier proves
+  // every wave has finished reading.
   GroupRegs r[NB];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (kseg > 0) issue(r[d], d, min(d * G, (kseg - 1) / G * G));
+  if (kseg > 0) issue(r[0], 0, 0);
   for (int k = 0; k < kseg; k += NB * G) {
     bool go = true;
     static_for<0, NB>([&](auto b_tag) {
@@ -1311,13 +1103,13 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
         go = false;
         return;
       }
-      // D - 1 groups were issued after group kk (past the last group the issue repeats the last
-      // group: L2 hits into a buffer nobody reads, so every step's count is the same)
+      // past the last group the issue repeats the last group: L2 hits into a buffer nobody reads,
+      // so every step's count is the same
       __builtin_amdgcn_sched_barrier(0);
-      qsgd_wait_vmcnt<(D - 1) * kOps>();
+      qsgd_wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      issue(r[(b + D) % NB], (b + D) % NB, min(kk + D * G, (kseg - 1) / G * G));
+      issue(r[(b + 1) % NB], (b + 1) % NB, min(kk + G, (kseg - 1) / G * G));
       run(b_tag, r[b], kk);
     });
   }
@@ -1329,24 +1121,14 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
 }
 
-// TILEN = 4096 (kTile1 table: every launch) or 8192 (kTileWide table, 512 lanes: whole-layout
-// launches — half the table traffic per element)
-template <int OUT, typename DQ, bool VEC, int TILEN = 4096>
-__global__ __launch_bounds__(TILEN == 4096 ? kQsgdLanes : TILEN / kQsgdAE)
-#if FEDAVG_QSGD_WPE
-__attribute__((amdgpu_waves_per_eu(FEDAVG_QSGD_WPE)))
-#endif
-void qsgd_tile_kernel(KArgs a) {
+template <int OUT, typename DQ, bool VEC>
+__global__ __launch_bounds__(kQsgdLanes) void qsgd_tile_kernel(KArgs a) {
   __shared__ double lut[kQsgdBufs][kQsgdGroup][kQsgdTable];
-  constexpr int kParts = TILEN == 4096 ? kQsgdTileLanes / kQsgdLanes : 1;  // workgroups per tile
-  const int bid = static_cast<int>(blockIdx.x);
-  const TileDesc td = load_tile(a.tiles, a.tile_begin + bid / kParts);
-  const int lane_base = (bid % kParts) * kQsgdLanes;
-  if (kParts > 1 && lane_base * kQsgdAE >= td.count) return;  // a quarter past a short tile's end
-  if (td.count == TILEN) {
-    qsgd_tile_body<OUT, DQ, true, VEC, TILEN>(a, td, lut, lane_base);
+  const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
+  if (td.count == kTile1) {
+    qsgd_tile_body<OUT, DQ, true, VEC>(a, td, lut);
   } else {
-    qsgd_tile_body<OUT, DQ, false, VEC, TILEN>(a, td, lut, lane_base);
+    qsgd_tile_body<OUT, DQ, false, VEC>(a, td, lut);
   }
 }
 
@@ -1395,16 +1177,9 @@ __global__ __launch_bounds__(kThreads) void qsgd_nan_scan_kernel(const TileDesc*
 constexpr int kNnadqHeader = 32;
 constexpr int kNnadqLanes = 256;
 constexpr int kNnadqAE = 16;
-#ifndef FEDAVG_NNADQ_GROUP
-#define FEDAVG_NNADQ_GROUP 2
-#endif
-constexpr int kNnadqGroup = FEDAVG_NNADQ_GROUP;
-#ifndef FEDAVG_NNADQ_ASM
-#define FEDAVG_NNADQ_ASM 0  // 1: inline-asm code loads + counted vmcnt waits (measured slower)
-#endif
-#ifndef FEDAVG_NNADQ_PK
-#define FEDAVG_NNADQ_PK 0  // 1: packed fp32 dequantisation (v_pk_mul_f32 / v_pk_add_f32; measured slower)
-#endif
+// 2-client groups (80 VGPRs, 6 waves per SIMD); inline-asm code loads with counted waits and a
+// packed fp32 dequantisation were measured slower and are not kept
+constexpr int kNnadqGroup = 2;
 static_assert(kNnadqLanes * kNnadqAE == kTile1, "NNADQ launches walk the 4096-element tile table");
 
 template <typename DQ>
@@ -1439,27 +1214,6 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
     DQ lo[G], step[G];  // wave-uniform (SGPRs): record header
     double wk[G];
   };
-#if FEDAVG_NNADQ_ASM
-  // Inline-asm code loads, every wave G of them per group (a short group repeats its last
-  // client, lanes past the tile's end load the record's first bytes): the compiler tracks none
-  // of them, so it inserts no vmcnt(0) between groups (its loop-carried tracking otherwise
-  // drained the next group's loads before every fold, measured by the ISA); the counted waits
-  // in the loop below retire each group right before its fold.
-  const int64_t code_off_any = lane_live ? code_off : 0;
-  auto issue = [&](GroupRegs& r, int k) {
-    const int n = min(G, kseg - k);  // wave-uniform
-#pragma unroll
-    for (int c = 0; c < G; ++c) {
-      const int kc = k + min(c, n - 1);
-      const uint64_t rec = cp[kc];
-      const kptr<double> hdr = to_const<double>(reinterpret_cast<const void*>(rec));
-      r.lo[c] = static_cast<DQ>(hdr[0]);
-      r.step[c] = static_cast<DQ>(hdr[1]);
-      r.wk[c] = wp[kc];
-      asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r.codes[c]) : "v"(rec + code_off_any) : "memory");
-    }
-  };
-#else
   auto issue = [&](GroupRegs& r, int k) {
     const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
@@ -1472,41 +1226,18 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
         r.wk[c] = wp[k + c];
         if (lane_live) {
           const gptr<const uint8_t> rp = to_global<uint8_t>(reinterpret_cast<const void*>(rec));
-#if FEDAVG_NT
           r.codes[c] = __builtin_nontemporal_load((gptr<const u32x4>)(rp + code_off));
-#else
-          r.codes[c] = *(gptr<const u32x4>)(rp + code_off);
-#endif
         } else {
           r.codes[c] = u32x4{0u, 0u, 0u, 0u};
         }
       }
     }
   };
-#endif
   auto run = [&](const GroupRegs& r, int k) {
     const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c < n) {
-#if FEDAVG_NNADQ_PK
-        if constexpr (std::is_same<DQ, float>::value) {
-          // fp32 codec: two elements per v_pk_mul_f32 / v_pk_add_f32 (each lane of the pair
-          // rounds on its own, exactly as the scalar code * step, + lo)
-          const f32x2 st2 = {r.step[c], r.step[c]};
-          const f32x2 lo2 = {r.lo[c], r.lo[c]};
-#pragma unroll
-          for (int j = 0; j < AE; j += 2) {
-            const uint32_t word = r.codes[c][j >> 2];
-            const f32x2 cc = {static_cast<float>((word >> (8 * (j & 3))) & 0xffu),
-                              static_cast<float>((word >> (8 * ((j + 1) & 3))) & 0xffu)};
-            const f32x2 v = cc * st2 + lo2;
-            acc[j] = fold<FOLD>(acc[j], static_cast<double>(v.x), r.wk[c], 0.0);
-            acc[j + 1] = fold<FOLD>(acc[j + 1], static_cast<double>(v.y), r.wk[c], 0.0);
-          }
-          continue;
-        }
-#endif
 #pragma unroll
         for (int j = 0; j < AE; ++j) {
           const uint32_t code = (r.codes[c][j >> 2] >> (8 * (j & 3))) & 0xffu;
@@ -1517,31 +1248,6 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
   };
   GroupRegs r0, r1;
   if (kseg > 0) issue(r0, 0);
-#if FEDAVG_NNADQ_ASM
-  // group i's loads retire with vmcnt(G) when group i + 1's G loads were issued after them,
-  // vmcnt(0) otherwise
-  auto retire = [&](bool next_issued) {
-    __builtin_amdgcn_sched_barrier(0);
-    if (next_issued) {
-      __builtin_amdgcn_s_waitcnt((G & 15) | ((G >> 4) << 14) | (7 << 4) | (15 << 8));
-    } else {
-      __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  for (int k = 0; k < kseg; k += 2 * G) {
-    const bool second = k + G < kseg;
-    if (second) issue(r1, k + G);
-    retire(second);
-    run(r0, k);
-    if (second) {
-      const bool third = k + 2 * G < kseg;
-      if (third) issue(r0, k + 2 * G);
-      retire(third);
-      run(r1, k + G);
-    }
-  }
-#else
   for (int k = 0; k < kseg; k += 2 * G) {
     const bool second = k + G < kseg;
     if (second) issue(r1, k + G);
@@ -1551,7 +1257,6 @@ __device__ __forceinline__ void nnadq_tile_body(const KArgs& a, const TileDesc& 
       run(r1, k + G);
     }
   }
-#endif
   have = have || (kseg > 0);
   if (!have) return;
   record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
@@ -1924,7 +1629,6 @@ struct fedavg_ctx {
 
   int split_policy = 1;  // 1 exact client order (default), 0 auto, 2 always split
   bool allow_fma = true;  // fused fold when every product is provably exact
-  int persistent_blocks = 0;  // grid cap of the exact-order kernel (0 = one block per tile)
   // whole-layout launches use the wide tile table only when they fold at least this many clients
   // per segment (short waves keep the 4096-element tiles: two workgroups per CU instead of one)
   int wide_min_clients = 0;
@@ -2282,7 +1986,7 @@ hipError_t launch_typed(const KArgs& a, int split, bool vec, int fold, int nbloc
     return vec ? launch_fold<T, OUT, 4, true>(a, fold, nblocks, s, e0, e1)
                : launch_fold<T, OUT, 4, false>(a, fold, nblocks, s, e0, e1);
   }
-  if constexpr ((sizeof(T) < 8 || FEDAVG_F64_WIDE) && kTileWide > 0) {
+  if constexpr (sizeof(T) < 8 && kTileWide > 0) {
     if (wide) {
       return vec ? launch_fold<T, OUT, 1, true, kTileWide>(a, fold, nblocks, s, e0, e1, partv)
                  : launch_fold<T, OUT, 1, false, kTileWide>(a, fold, nblocks, s, e0, e1);
@@ -2326,7 +2030,7 @@ hipError_t launch_nnadq_out(int32_t in_dtype, const KArgs& a, bool vec, bool fma
 
 template <int OUT>
 hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream_t s, hipEvent_t e1, int32_t seg_begin,
-                           int32_t seg_count, bool wide = false) {
+                           int32_t seg_count) {
   // the call's |product| tables first (same stream: the tile kernel reads them by DMA)
   const dim3 tgrid(static_cast<unsigned>(a.K), static_cast<unsigned>(seg_count));
   if (in_dtype == FEDAVG_QSGD_F32)
@@ -2335,20 +2039,7 @@ hipError_t launch_qsgd_out(int32_t in_dtype, const KArgs& a, bool vec, hipStream
   else
     hipLaunchKernelGGL(qsgd_table_kernel<double>, tgrid, dim3(kQsgdSlots), 0, s, a.tab, a.K, seg_begin,
                        const_cast<double*>(a.qtab));
-  if constexpr (FEDAVG_QSGD_WIDE && kTileWide == 8192 && !FEDAVG_QSGD_SOLO) {
-    if (wide) {  // a.tiles is the kTileWide table
-      const dim3 gw(static_cast<unsigned>(a.num_tiles)), bw(8192 / kQsgdAE);
-      if (in_dtype == FEDAVG_QSGD_F32) {
-        if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
-        else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, false, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
-      } else {
-        if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, double, true, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
-        else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, double, false, 8192>), gw, bw, 0, s, nullptr, e1, 0, a);
-      }
-      return hipGetLastError();
-    }
-  }
-  const dim3 grid(static_cast<unsigned>(a.num_tiles * (kQsgdTileLanes / kQsgdLanes))), block(kQsgdLanes);
+  const dim3 grid(static_cast<unsigned>(a.num_tiles)), block(kQsgdLanes);
   if (in_dtype == FEDAVG_QSGD_F32) {
     if (vec) hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, true>), grid, block, 0, s, nullptr, e1, 0, a);
     else hipExtLaunchKernelGGL((qsgd_tile_kernel<OUT, float, false>), grid, block, 0, s, nullptr, e1, 0, a);
@@ -2373,11 +2064,16 @@ int choose_split(const fedavg_ctx* c, int kmax) {
 // profiling is on, the profiling stop event is handed back in its place.
 int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_dtype, int out_kind,
                     int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1,
-                    hipEvent_t* done_ev = nullptr, double* acc_out = nullptr) {
+                    hipEvent_t* done_ev = nullptr, double* acc_out = nullptr,
+                    const KArgs* win = nullptr) {
   if (st.delta) split = 1;  // delta folds run the exact-order kernel only
   KArgs a;
   a.segs = c->d_segs;
   a.tab = st.tab;
+  // win (dense zero-initialised partials only): the multi-device window table (KArgs::win_dst)
+  a.win_dst = win ? win->win_dst : nullptr;
+  a.win_edge = win ? win->win_edge : nullptr;
+  a.win_n = win ? win->win_n : 0;
   // acc_out: a zero-initialised partial written elsewhere in accumulator coordinates (the
   // multi-device exchange: another device's receive slot, through the peer mapping)
   a.acc = acc_out ? acc_out : c->acc;
@@ -2398,11 +2094,12 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     te = te_split1;
   }
   // whole-layout exact-order launch of a 2- / 4-byte input: the wide table (same elements)
-  const bool wide = split == 1 && c->d_tilesw != nullptr && c->persistent_blocks == 0 && tb_split1 == 0 &&
+  // (a windowed launch indexes the exact-order table: no wide / balanced / reversed orders)
+  const bool wide = !win && split == 1 && c->d_tilesw != nullptr && tb_split1 == 0 &&
                     st.Kmax >= c->wide_min_clients &&
                     te_split1 == static_cast<int32_t>(c->tiles1.size()) &&
                     (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F16 || in_dtype == FEDAVG_BF16 ||
-                     (FEDAVG_F64_WIDE && in_dtype == FEDAVG_F64));
+                     false);
   if (wide) {
     a.tiles = c->d_tilesw;
     tb = 0;
@@ -2411,7 +2108,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
       a.tiles = c->d_tilesw_bal;
       te = static_cast<int>(c->tilesw_bal.size());
     }
-  } else if (split == 1 && in_dtype == FEDAVG_F64 && c->d_tiles1_bal != nullptr && c->persistent_blocks == 0 &&
+  } else if (!win && split == 1 && in_dtype == FEDAVG_F64 && c->d_tiles1_bal != nullptr &&
              tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
     a.tiles = c->d_tiles1_bal;  // a whole-layout fp64 launch: the balanced order of the same tiles
     tb = 0;
@@ -2423,7 +2120,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   // whole-layout waves alternate their walk (a balanced order reverses only its leading whole
   // waves: its short pieces stay at the end, where they balance the tail; ranged launches keep
   // their order)
-  if (c->walk_alternate && split == 1 && c->persistent_blocks == 0 && !is_record(in_dtype) &&
+  if (!win && c->walk_alternate && split == 1 && !is_record(in_dtype) &&
       tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
     if (c->walk_reverse)
       a.walk_back = (a.tiles == c->d_tilesw_bal)   ? c->tilesw_bal_head
@@ -2431,9 +2128,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
                                                    : a.num_tiles;
     if (out_kind == OUT_ACC) c->walk_reverse = !c->walk_reverse;
   }
-  // exact-order kernel: persistent grid of at most (resident blocks) workgroups
-  const int nblocks = (split == 1 && c->persistent_blocks > 0) ? std::min(a.num_tiles, c->persistent_blocks)
-                                                               : a.num_tiles;
+  const int nblocks = a.num_tiles;
   // Profiling events are recorded as markers around the launch (the cheapest form measured:
   // attaching start/stop events to the dispatch cost the fused step ~6 µs more); without
   // profiling, a requested done event is attached to the dispatch itself (no marker).
@@ -2448,9 +2143,9 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     e1 = nullptr;
   }
   hipError_t err = hipSuccess;
+  if (is_record(in_dtype) && win) return fail(FEDAVG_ERR_INVALID, "windowed launches take dense inputs");
   if (is_record(in_dtype)) {
-    // quantised records: one tile per workgroup, exact client order (no split, no persistent
-    // grid); the record layout needs 16-B aligned records; outputs may be unaligned
+    // quantised records: one tile per workgroup, exact client order (no split); the record layout needs 16-B aligned records; outputs may be unaligned
     if (st.delta) return fail(FEDAVG_ERR_INVALID, "quantised records cannot be delta updates");
     if (!st.clients_aligned) return fail(FEDAVG_ERR_INVALID, "quantised records must be 16-byte aligned");
     a.tiles = c->d_tiles1;
@@ -2487,18 +2182,10 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     a.qtab = c->qtab;
     const int32_t seg0 = c->tiles1[tb_split1].seg;
     const int32_t nseg = c->tiles1[te_split1 - 1].seg - seg0 + 1;
-    // a whole-layout launch folds the 8192-element tiles (half the table traffic per element)
-    const bool qwide = FEDAVG_QSGD_WIDE && c->d_tilesw != nullptr && tb_split1 == 0 &&
-                       te_split1 == static_cast<int32_t>(c->tiles1.size());
-    if (qwide) {
-      a.tiles = c->d_tilesw;
-      a.tile_begin = 0;
-      a.num_tiles = static_cast<int>(c->tilesw.size());
-    }
     switch (out_kind) {
-      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1, seg0, nseg, qwide); break;
-      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1, seg0, nseg, qwide); break;
-      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1, seg0, nseg, qwide); break;
+      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
+      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
+      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
       default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
     }
     if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
@@ -2574,7 +2261,7 @@ extern "C" {
 int32_t fedavg_abi_version(void) { return FEDAVG_ABI_VERSION; }
 
 int32_t fedavg_build_flags(void) {
-  return (FEDAVG_ABLATE_EPILOGUE ? FEDAVG_BUILD_ABLATE_EPILOGUE : 0) | (FEDAVG_QSGD_ABLATE ? FEDAVG_BUILD_ABLATE_QSGD : 0);
+  return 0;  // the timing-only ablation variants are no longer part of the sources
 }
 
 int32_t fedavg_kernel_constant(const char* name, int64_t* out) {
@@ -2599,7 +2286,7 @@ int32_t fedavg_kernel_constant(const char* name, int64_t* out) {
     const std::string d = dsep == std::string::npos ? "" : n.substr(dsep + 1);
     auto pick = [&](auto tag) {
       using T = decltype(tag);
-      using GW = Geo<T, 1, ((sizeof(T) < 8 || FEDAVG_F64_WIDE) && kTileWide > 0) ? kTileWide : kTile1>;
+      using GW = Geo<T, 1, (sizeof(T) < 8 && kTileWide > 0) ? kTileWide : kTile1>;
       using G1 = Geo<T, 1, kTile1>;
       constexpr int VPLW = GW::AE / Vec16<T>::n;
       constexpr int CU_B = sizeof(T) == 8 ? FEDAVG_CU_BYTES_F64 : FEDAVG_CU_BYTES;
@@ -2707,19 +2394,6 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
                                  static_cast<int64_t>(per_cu) * cus, c->tiles1_bal);
     }
   }
-#if FEDAVG_PERSISTENT
-  {
-    int per_cu = 0, cus = 0;
-    hipDeviceProp_t prop;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void*>(&fedavg_tile_kernel<float, OUT_F32, 1, true, FOLD_FMA>),
-            Geo<float, 1>::THREADS, 0) == hipSuccess &&
-        hipGetDeviceProperties(&prop, device) == hipSuccess) {
-      cus = prop.multiProcessorCount;
-      c->persistent_blocks = std::max(1, per_cu) * cus;
-    }
-  }
-#endif
   if (c->tiles1.size() > static_cast<size_t>(INT32_MAX / 2)) {
     delete c;
     return fail(FEDAVG_ERR_INVALID, "layout too large");
@@ -3474,6 +3148,32 @@ __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range_to(
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, 1, tb, te, nullptr,
                      acc_out);
+}
+
+// Shared with multi_device.cpp: one launch of a zero-initialised dense partial plan over tiles
+// [tb, te) whose tiles store into the window table's destinations (device tables: dst[n] slot
+// pointers, edge[n + 1] absolute tile edges). FEDAVG_ERR_INVALID for record plans (the caller then
+// launches window by window through fedavg_internal_plan_run_range_to).
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_windows(fedavg_plan* p, int32_t tb, int32_t te,
+                                                                             void* stream, double* const* dst,
+                                                                             const int32_t* edge, int32_t n) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind != fedavg_plan::PARTIAL || !p->zero_init)
+    return fail(FEDAVG_ERR_INVALID, "the multi-device exchange takes zero-initialised partial plans");
+  if (is_record(p->in_dtype)) return fail(FEDAVG_ERR_INVALID, "windowed launches take dense inputs");
+  fedavg_ctx* c = p->ctx;
+  const int32_t nt = static_cast<int32_t>(c->tiles1.size());
+  if (tb < 0 || tb > te || te > nt || n < 1) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  KArgs win{};
+  win.win_dst = dst;
+  win.win_edge = edge;
+  win.win_n = n;
+  return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, 1, tb, te, nullptr,
+                     nullptr, &win);
+}
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_is_record(const fedavg_plan* p) {
+  return (p && is_record(p->in_dtype)) ? 1 : 0;
 }
 
 // Shared with multi_device.cpp: the device-ordered sum of G fp64 partials over tiles [tb, te) of

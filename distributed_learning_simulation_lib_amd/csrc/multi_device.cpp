@@ -7,9 +7,10 @@
 // high-priority exchange stream per entry, and the peer mappings between the devices.
 //
 // The PEER exchange (no collective library): chunk k of the tile table is cut into G windows and
-// device j owns window j. Per chunk, device g runs its partial kernel once per window, each writing
-// its fp64 partial of window j straight into device j's receive slot for g over xGMI (the store
-// address is a peer mapping; device g's own window goes last, into its own slot). An event after
+// device j owns window j. Per chunk, device g runs one partial launch over the chunk whose tiles of
+// window j store their fp64 partial straight into device j's receive slot for g over xGMI (the
+// store address is a peer mapping picked per tile from a window table; device g's own window goes
+// into its own slot). An event after
 // device g's chunk k orders the exchange stream of every device j behind it; device j's exchange
 // stream then sums the G partials of its window in device order, divides and stores the result
 // into the root's outputs (a peer store for j != root). Per round, HBM carries on each device its
@@ -18,7 +19,7 @@
 // engine or collective kernel sits between the fold and the division.
 //
 //   exchange stream j : (wait part[0..G-1][k]) combine(window j of chunk k) ... -> done[j]
-//   stream g          : partial(chunk k, window g+1) ... partial(chunk k, window g) -> part[g][k]
+//   stream g          : partial(chunk k: every window to its owner's slot) -> part[g][k]
 //
 // The REDUCE exchange keeps the per-process path's arithmetic: each chunk's partial is reduced to
 // the root's accumulator by an in-process RCCL communicator (ncclCommInitAll, grouped calls from
@@ -40,6 +41,10 @@ __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range(fed
                                                                            void* stream, hipEvent_t* done_ev);
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_range_to(fedavg_plan* p, int32_t tb, int32_t te,
                                                                               void* stream, double* acc_out);
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_windows(fedavg_plan* p, int32_t tb, int32_t te,
+                                                                             void* stream, double* const* dst,
+                                                                             const int32_t* edge, int32_t n);
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_is_record(const fedavg_plan* p);
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_multi_combine(fedavg_ctx* c, int32_t tb, int32_t te,
                                                                           const double* const* slots, int32_t G,
                                                                           const double* wtot, void* const* outs,
@@ -86,6 +91,11 @@ struct fedavg_multi {
   std::vector<hipEvent_t> start_ev;   // the caller's stream g, at round start
   std::vector<hipEvent_t> done_ev;    // entry j's last exchange work of the round
   std::vector<std::vector<hipEvent_t>> part_ev;  // [g][chunk]
+  // per entry g: its window table for the windowed partial launches — G slot pointers (device j's
+  // receive slot for g) then [chunks][G + 1] tile edges — on device g, and its host image
+  std::vector<char*> win_dev;
+  std::vector<size_t> win_cap;
+  std::vector<std::vector<char>> win_host;
   bool any_round = false;
   // in-process RCCL (REDUCE exchange)
   std::vector<ncclComm_t> nccl;
@@ -135,6 +145,34 @@ int32_t upload_tables(fedavg_multi* m, const double* totals, void* const* outs) 
     if (!m->tab_dev[j]) MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->tab_dev[j]), img.size()));
     MULTI_HIP_TRY(hipMemcpy(m->tab_dev[j], img.data(), img.size(), hipMemcpyHostToDevice));
     m->tab_host[j] = img;
+  }
+  return FEDAVG_OK;
+}
+
+// Entry g's window table for this round's chunk edges (re-uploaded only when the edges change, after
+// the device finished the launches that read the old one).
+int32_t upload_windows(fedavg_multi* m, const std::vector<int32_t>& edges) {
+  const int32_t G = m->G, chunks = static_cast<int32_t>(edges.size()) - 1;
+  for (int32_t g = 0; g < G; ++g) {
+    std::vector<char> img(sizeof(double*) * G + sizeof(int32_t) * static_cast<size_t>(chunks) * (G + 1));
+    for (int32_t j = 0; j < G; ++j) std::memcpy(img.data() + sizeof(double*) * j, &m->slots[j][g], sizeof(double*));
+    auto* e = reinterpret_cast<int32_t*>(img.data() + sizeof(double*) * G);
+    for (int32_t k = 0; k < chunks; ++k) {
+      const int64_t tb = edges[k], span = edges[k + 1] - edges[k];
+      for (int32_t j = 0; j <= G; ++j) e[k * (G + 1) + j] = static_cast<int32_t>(tb + span * j / G);
+    }
+    if (m->win_host[g] == img) continue;
+    MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
+    MULTI_HIP_TRY(hipDeviceSynchronize());
+    if (m->win_cap[g] < img.size()) {
+      if (m->win_dev[g]) MULTI_HIP_TRY(hipFree(m->win_dev[g]));
+      m->win_dev[g] = nullptr;
+      m->win_cap[g] = 0;
+      MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->win_dev[g]), img.size()));
+      m->win_cap[g] = img.size();
+    }
+    MULTI_HIP_TRY(hipMemcpy(m->win_dev[g], img.data(), img.size(), hipMemcpyHostToDevice));
+    m->win_host[g] = img;
   }
   return FEDAVG_OK;
 }
@@ -260,6 +298,9 @@ int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t 
   m->start_ev.assign(m->G, nullptr);
   m->done_ev.assign(m->G, nullptr);
   m->part_ev.assign(m->G, {});
+  m->win_dev.assign(m->G, nullptr);
+  m->win_cap.assign(m->G, 0);
+  m->win_host.assign(m->G, {});
   auto bail = [&](int32_t st) {
     fedavg_multi_destroy(m);
     return st;
@@ -323,6 +364,7 @@ int32_t fedavg_multi_destroy(fedavg_multi* m) {
     for (int32_t g = 0; g < m->G; ++g)
       if (m->slot_owned[j][g] && m->slots[j][g]) (void)hipFree(m->slots[j][g]);
     if (m->tab_dev[j]) (void)hipFree(m->tab_dev[j]);
+    if (m->win_dev[j]) (void)hipFree(m->win_dev[j]);
     for (hipEvent_t ev : m->part_ev[j]) (void)hipEventDestroy(ev);
     if (m->start_ev[j]) (void)hipEventDestroy(m->start_ev[j]);
     if (m->done_ev[j]) (void)hipEventDestroy(m->done_ev[j]);
@@ -377,6 +419,7 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
     if (int32_t st = ensure_slots(m)) return st;
     if (int32_t st = ensure_part_events(m, chunks)) return st;
     if (int32_t st = upload_tables(m, total_weights, out_ptrs)) return st;
+    if (int32_t st = upload_windows(m, edges)) return st;
     if (int32_t st = order_round_start(m, streams)) return st;
     const int32_t vec = outs_aligned(out_ptrs, m->T, out_dtype) ? 1 : 0;
     for (int32_t k = 0; k < chunks; ++k) {
@@ -388,12 +431,21 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
       for (int32_t g : members) {
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
         hipStream_t s = stream_of(m, streams, g);
-        for (int32_t r = 1; r <= m->G; ++r) {
-          const int32_t j = (g + r) % m->G;  // the owner's window; this device's own goes last
-          int32_t wb = 0, we = 0;
-          window(j, wb, we);
-          if (wb == we) continue;
-          if (int32_t st = fedavg_internal_plan_run_range_to(partials[g], wb, we, s, m->slots[j][g])) return st;
+        if (!fedavg_internal_plan_is_record(partials[g])) {
+          // one launch over the chunk: each tile stores into its window owner's slot
+          const char* wt = m->win_dev[g];
+          if (int32_t st = fedavg_internal_plan_run_windows(
+                  partials[g], edges[k], edges[k + 1], s, reinterpret_cast<double* const*>(wt),
+                  reinterpret_cast<const int32_t*>(wt + sizeof(double*) * m->G) + k * (m->G + 1), m->G))
+            return st;
+        } else {
+          for (int32_t r = 1; r <= m->G; ++r) {
+            const int32_t j = (g + r) % m->G;  // quantised records: one launch per window, own last
+            int32_t wb = 0, we = 0;
+            window(j, wb, we);
+            if (wb == we) continue;
+            if (int32_t st = fedavg_internal_plan_run_range_to(partials[g], wb, we, s, m->slots[j][g])) return st;
+          }
         }
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
         MULTI_HIP_TRY(hipEventRecord(m->part_ev[g][k], s));

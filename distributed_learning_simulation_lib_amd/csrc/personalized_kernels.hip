@@ -79,21 +79,10 @@ static_assert(kJB == 8 || kJB == 16, "receivers per wave");
 #define PERS_U 2
 #endif
 constexpr int kU = PERS_U;             // clients loaded ahead per lane
-#ifndef PERS_RING  // 1: whole aligned fp32/fp64 chunks stream clients through an LDS-DMA ring
-#define PERS_RING 1
-#endif
-#ifndef PERS_RING_UNROLL  // clients of a ring stage folded per unrolled step (VGPR pressure)
-#define PERS_RING_UNROLL 1
-#endif
-#ifndef PERS_RING_WEIGHTS  // 1: the ring stages carry each wave's weight rows too (LDS broadcast reads)
-#define PERS_RING_WEIGHTS 0
-#endif
-#ifndef PERS_RING_MULADD  // 1: the mul + add fold (float weights) streams through the ring as well
-#define PERS_RING_MULADD 0
-#endif
-#ifndef PERS_PREFETCH  // 1: the ring loop loads client k + 1's weight row (and ring slice) under client k's folds
-#define PERS_PREFETCH 0
-#endif
+// Whole aligned fp32 / fp64 chunks of the fused (FMA) fold stream clients through an LDS-DMA ring;
+// the separately rounded fold keeps the register pipeline (VALU-bound: the ring measured 3 % slower
+// there). Weight rows staged through the ring, and a one-client-ahead weight prefetch, measured
+// slower and are not kept.
 
 struct PChunk {
   int32_t seg;
@@ -314,7 +303,6 @@ __device__ __forceinline__ void store_result(uint64_t op, int64_t start, int e, 
 constexpr int kSC = 4;   // clients per stage
 constexpr int kD = 3;    // stages in flight ahead of the one being folded
 constexpr int kRS = kD + 2;  // ring stages: the stage being written was last read two barriers ago
-constexpr int kRingUnroll = PERS_RING_UNROLL;
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_le() {
@@ -368,16 +356,6 @@ struct Glds<float> {
     x[2] = v.z;
     x[3] = v.w;
   }
-  using RawT = f32x4;  // the slice as read (widened only where it is folded)
-  __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
-    return *reinterpret_cast<const f32x4*>(slot + lane * 16);
-  }
-  __device__ __forceinline__ static void expand(const RawT& v, double* x) {
-    x[0] = v.x;
-    x[1] = v.y;
-    x[2] = v.z;
-    x[3] = v.w;
-  }
 };
 template <>
 struct Glds<double> {
@@ -398,16 +376,6 @@ struct Glds<double> {
     x[2] = hi.x;
     x[3] = hi.y;
   }
-  using RawT = f64x2x2;
-  __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
-    return RawT{*reinterpret_cast<const f64x2*>(slot + lane * 16), *reinterpret_cast<const f64x2*>(slot + 1024 + lane * 16)};
-  }
-  __device__ __forceinline__ static void expand(const RawT& v, double* x) {
-    x[0] = v.lo.x;
-    x[1] = v.lo.y;
-    x[2] = v.hi.x;
-    x[3] = v.hi.y;
-  }
 };
 template <typename T>
 constexpr bool kHasGlds = std::is_same<T, float>::value || std::is_same<T, double>::value;
@@ -425,17 +393,6 @@ __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, in
   // the others none) — each wave waits for its own DMAs only, the barrier for the rest
   const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
   const int nst = a.Npad / kSC;
-#if PERS_RING_WEIGHTS
-  // Each stage also carries this wave's 16 weights of each of its kSC clients (kSC x 128 B): one
-  // more DMA per wave and stage (lanes 0-31; lanes 32-63 repeat them into a copy nobody reads).
-  // The fold then reads them from LDS (broadcast reads) instead of waiting on scalar loads
-  // from L2 for every client — the weight row is in LDS a few stages before it is needed.
-  char* const wring = ring + kRS * kSC * G::kSlice;  // [kRS][waves][1 KiB]
-  const double* const wsrc = a.w + wave * kJB + 2 * (lane & 7);
-  constexpr int kWIPS = 1;  // weight DMAs per wave and stage
-#else
-  constexpr int kWIPS = 0;
-#endif
   auto issue = [&](int st) {
     char* stage = ring + (st % kRS) * (kSC * G::kSlice);
     for (int i = 0; i < per; ++i) {
@@ -443,77 +400,19 @@ __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, in
       const uint64_t p = ptrs[st * kSC + c];
       G::issue(p ? p + sb : zeros, lane, stage + c * G::kSlice);
     }
-#if PERS_RING_WEIGHTS
-    const int c = (lane >> 3) & (kSC - 1);
-    __builtin_amdgcn_global_load_lds((void PERS_AS_GLOBAL*)(wsrc + static_cast<int64_t>(st * kSC + c) * a.wstride),
-                                     (void __attribute__((address_space(3)))*)(wring + ((st % kRS) * waves + wave) * 1024),
-                                     16, 0, 0);
-#endif
   };
   for (int st = 0; st < kD && st < nst; ++st) issue(st);
-#if PERS_PREFETCH && !PERS_RING_WEIGHTS
-  // Software pipeline, one client ahead: client k + 1's weight row (SGPRs, s_load from L2) and
-  // — inside a stage — its ring slice (ds_read) are issued before client k's 64 folds, and one
-  // explicit lgkmcnt(0) after the folds retires both (the compiler would otherwise wait for the
-  // weights right after issuing them: SMEM returns out of order, so any LDS wait is lgkmcnt(0)).
-  double wc[kJB], wn[kJB];
-#pragma unroll
-  for (int j = 0; j < kJB; ++j) wc[j] = wt[j];
-  typename G::RawT rc, rn;
-  for (int st = 0; st < nst; ++st) {
-    if (st + kD < nst) issue(st + kD);
-    const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;
-    wait_vmcnt(ahead * (per * G::kIPC + kWIPS));
-    __builtin_amdgcn_s_barrier();
-    const char* stage = ring + (st % kRS) * (kSC * G::kSlice);
-    rc = G::read_raw(stage, lane);
-    __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));  // lgkmcnt(0)
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < kSC; ++c) {
-      const int k = st * kSC + c;
-      const int kn = (k + 1 < a.Npad) ? k + 1 : k;
-      const kp<double> wk = wt + static_cast<int64_t>(kn) * a.wstride;
-      double xc[kVE];
-      G::expand(rc, xc);  // client k's slice: retired by the wait at the end of client k - 1
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < kJB; ++j) wn[j] = wk[j];
-      if (c + 1 < kSC) rn = G::read_raw(stage + (c + 1) * G::kSlice, lane);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < kJB; ++j) {
-#pragma unroll
-        for (int v = 0; v < kVE; ++v) acc[v][j] = pfold<FOLD>(acc[v][j], xc[v], wc[j]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));  // lgkmcnt(0)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < kJB; ++j) wc[j] = wn[j];
-      if (c + 1 < kSC) rc = rn;
-    }
-  }
-  return;
-#endif
   for (int st = 0; st < nst; ++st) {
     if (st + kD < nst) issue(st + kD);
     const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;  // stages issued after st
-    wait_vmcnt(ahead * (per * G::kIPC + kWIPS));  // this wave's slices of stage st have landed
+    wait_vmcnt(ahead * per * G::kIPC);  // this wave's slices of stage st have landed
     __builtin_amdgcn_s_barrier();        // ... and every other wave's
     const char* stage = ring + (st % kRS) * (kSC * G::kSlice);
-#if PERS_RING_WEIGHTS
-    const double* const wst = reinterpret_cast<const double*>(wring + ((st % kRS) * waves + wave) * 1024);
-#endif
-#pragma unroll kRingUnroll
+#pragma unroll 1
     for (int c = 0; c < kSC; ++c) {
       double x[kVE];
       G::read(stage + c * G::kSlice, lane, x);
-#if PERS_RING_WEIGHTS
-      const double* wk = wst + c * kJB;
-#else
       const kp<double> wk = wt + static_cast<int64_t>(st * kSC + c) * a.wstride;
-#endif
 #pragma unroll
       for (int j = 0; j < kJB; ++j) {
         const double wj = wk[j];
@@ -1086,10 +985,10 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
     // the LDS ring (whole aligned fp32 / fp64 chunks) for the fused fold: measured 3.08 -> 2.85 ms
     // (64 x 64 ResNet-18); the mul + add fold is VALU-bound and ~3 % faster on the register
     // pipeline, which every other case keeps
-    a.ring = PERS_RING && (fold == PF_FMA || PERS_RING_MULADD) && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
+    a.ring = fold == PF_FMA && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
     const size_t slice = static_cast<size_t>(kChunk) * (in_dtype == FEDAVG_F64 ? 8 : 4);
     const size_t lds = sizeof(double) * 64 * kVE +
-                       (a.ring ? kRS * kSC * slice + (PERS_RING_WEIGHTS ? kRS * 1024 * static_cast<size_t>(a.waves) : 0) : 0);
+                       (a.ring ? kRS * kSC * slice : 0);
     const hipError_t err = launch_pers(in_dtype, a, fold, nchunks, threads, lds, s);
     if (err != hipSuccess) return pfail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
     if (p->prof) {

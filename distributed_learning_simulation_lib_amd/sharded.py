@@ -350,10 +350,14 @@ class ExchangeModel:
     357 tiles +0.07 ms per one-rank round against 2-4 chunks)."""
 
     def __init__(self, fold_rate: float = 6.45e12, hbm_rate: float = 6.5e12, link_rate: float = 153e9,
-                 link_eff: float = 0.75, full_chunk_tiles: int = 512, underfill_ms: float = 0.009) -> None:
+                 link_eff: float = 0.75, full_chunk_tiles: int = 512, underfill_ms: float = 0.009,
+                 sync_ms: float = 0.008) -> None:
         self.fold_rate, self.hbm_rate = fold_rate, hbm_rate
         self.link_rate, self.link_eff = link_rate, link_eff
         self.full_chunk_tiles, self.underfill_ms = full_chunk_tiles, underfill_ms
+        # the peer exchange's cross-device hand-off after the last chunk (event marker, a peer's wait,
+        # the combine launch): assumed, not measurable on one GPU
+        self.sync_ms = sync_ms
 
     def one_gpu_ms(self, numel: int, n_clients: int, in_bytes: int, out_bytes: int) -> float:
         """The fused single-launch round on one GPU (the strong-scaling anchor)."""
@@ -376,6 +380,8 @@ class ExchangeModel:
         total_tiles = edges[-1]
         fracs = [(b - a) / total_tiles for a, b in zip(edges, edges[1:])]
         under = [self.underfill_ms if b - a < self.full_chunk_tiles else 0.0 for a, b in zip(edges, edges[1:])]
+        if exchange == "peer":
+            return self._peer_round_ms(G, numel, n_clients, in_bytes, out_bytes, fracs, under, n_root, n_peer)
         root_t = peer_t = x_end = 0.0
         xs, x_ends = [], []
         for c, f in enumerate(fracs):
@@ -405,6 +411,41 @@ class ExchangeModel:
         t1 = self.one_gpu_ms(numel, n_clients, in_bytes, out_bytes)
         return {"fold_ms": round(fold, 4), "exposed_exchange_and_finalize_ms": round(step - fold, 4),
                 "last_chunk_exchange_ms": round(xs[-1], 4), "last_finalize_ms": round(last_div, 4),
+                "root_clients": n_root, "peer_clients": n_peer,
+                "step_ms": round(step, 4), "one_gpu_ms": round(t1, 4), "speedup": round(t1 / step, 3)}
+
+    def _peer_round_ms(self, G: int, numel: int, n_clients: int, in_bytes: int, out_bytes: int, fracs: list[float],
+                       under: list[float], n_root: int, n_peer: int) -> dict[str, float]:
+        """The single-process peer-window exchange (multi_device.cpp). Per chunk every
+        device folds its clients window by window, its partial of window j stored straight into
+        device j's receive slot (a peer store: the link carries S/G per peer per round, the
+        receiver's HBM takes it), then device j sums its G slot windows of the chunk and divides,
+        storing 1/G of the result into the root. A device's HBM per chunk: its clients + its own
+        window's partial + the (G-1) windows arriving from peers + the previous chunk's combine
+        (G slot windows read) + on the root all result windows; the fold of a chunk cannot end
+        before its peer stores have drained over the links. After the last chunk: its combine,
+        the result windows' trip to the root over one link each, and a cross-device hand-off."""
+        link = self.link_rate * self.link_eff
+        rate = self.fold_rate / 1e3
+        part_b, res_b = numel * 8, numel * out_bytes
+        root_t = peer_t = 0.0
+        for c, f in enumerate(fracs):
+            combine_prev = fracs[c - 1] * part_b if c else 0.0  # G slot windows of the last chunk
+            recv = f * part_b  # its own window + (G-1) windows from the peers
+            clients_root, clients_peer = f * n_root * numel * in_bytes, f * n_peer * numel * in_bytes
+            drain = f * part_b / G / link * 1e3 if G > 1 else 0.0  # one window per peer link
+            root_t += max((clients_root + recv + combine_prev + (fracs[c - 1] * res_b if c else 0.0)) / rate,
+                          drain) + under[c]
+            peer_t += max((clients_peer + recv + combine_prev) / rate, drain) + under[c]
+        last = fracs[-1]
+        combine_last = (last * part_b + last * res_b / G) / rate
+        result_link = last * res_b / G / link * 1e3 if G > 1 else 0.0
+        fold = max(root_t, peer_t if G > 1 else 0.0)
+        tail = combine_last + result_link + (self.sync_ms if G > 1 else 0.0)
+        step = fold + tail
+        t1 = self.one_gpu_ms(numel, n_clients, in_bytes, out_bytes)
+        return {"fold_ms": round(fold, 4), "exposed_exchange_and_finalize_ms": round(tail, 4),
+                "last_chunk_exchange_ms": round(result_link, 4), "last_finalize_ms": round(combine_last, 4),
                 "root_clients": n_root, "peer_clients": n_peer,
                 "step_ms": round(step, 4), "one_gpu_ms": round(t1, 4), "speedup": round(t1 / step, 3)}
 
@@ -501,11 +542,13 @@ def sharded_reduce(
     return global_totals
 
 
-def exchange_candidates(chunks: int | None = None, shapes: Sequence[str] = CHUNK_SHAPES) -> list[tuple[str, int, str]]:
+def exchange_candidates(chunks: int | None = None, shapes: Sequence[str] = CHUNK_SHAPES,
+                        exchanges: Sequence[str] = ("reduce", "scatter")) -> list[tuple[str, int, str]]:
     """(exchange, chunks, shape) triples ``tune_exchange`` tries: both exchanges at 2 / 4 / 6 / 8
-    chunks (or the given count only), every chunk shape (one shape when there is one chunk)."""
+    chunks (or the given count only), every chunk shape (one shape when there is one chunk).
+    ``exchanges=("peer", "reduce")``: the single-process multi-device round's candidates."""
     out = []
-    for ex in ("reduce", "scatter"):
+    for ex in exchanges:
         for c in ((chunks,) if chunks else (2, 4, 6, 8)):
             for sh in (shapes if c > 1 else ("even",)):
                 out.append((ex, c, sh))

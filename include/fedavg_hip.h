@@ -106,7 +106,8 @@ typedef struct fedavg_ctx fedavg_ctx;
 int32_t fedavg_abi_version(void);
 
 /* Compile-time variants the library was built with: 0 for the product build. Non-zero bits
- * mark timing-only ablation builds whose results are WRONG by design (kernel A/B studies):
+ * mark timing-only ablation builds whose results are WRONG by design (the kernel A/B studies of
+ * rounds 1-3; their sources are no longer shipped, so this build always reports 0):
  * FEDAVG_BUILD_ABLATE_EPILOGUE (reciprocal multiply, no NaN checks), FEDAVG_BUILD_ABLATE_QSGD.
  * Bindings refuse to load such a build unless asked to (_native.py). */
 #define FEDAVG_BUILD_ABLATE_EPILOGUE 0x1

@@ -440,3 +440,22 @@ def test_tune_budget_stops_every_rank_after_the_same_candidate():
         assert p.exitcode == 0
     first = exchange_candidates()[0]
     assert got[0] == got[1] == (first, [first])
+
+
+def test_exchange_model_prices_the_peer_window_exchange():
+    """the single-process peer exchange writes no whole fp64 partial and has no
+    collective kernel; on the same assumptions it beats the RCCL schedules at every G."""
+    from distributed_learning_simulation_lib_amd.sharded import ExchangeModel
+
+    m = ExchangeModel()
+    P, tiles = 11_689_512, 2854
+    for G in (2, 4, 8):
+        (ex, ch, sh), peer = m.best(G, P, 256, 4, 4, tiles, exchange_candidates(exchanges=("peer",)))
+        _, rccl = m.best(G, P, 256, 4, 4, tiles)
+        assert ex == "peer" and peer["speedup"] > rccl["speedup"] and peer["speedup"] < G
+        assert peer["step_ms"] >= peer["fold_ms"] > 0
+    (_, _, _), p4 = m.best(4, P, 256, 4, 4, tiles, exchange_candidates(exchanges=("peer",)))
+    assert p4["speedup"] >= 3.5
+    # no link at all on one device: the fold alone plus the combine
+    one = m.round_ms(1, P, 256, 4, 4, [0, tiles], "peer")
+    assert one["last_chunk_exchange_ms"] == 0.0

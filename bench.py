@@ -823,6 +823,13 @@ def main_qsgd(args: argparse.Namespace) -> int:
         "hbm_probe": probe,
         "cpu_baseline": cpu,
     }
+    if not nnadq:
+        # the |product| tables qsgd_table_kernel builds per launch (K clients x 256 fp64 per segment,
+        # launches split at FEDAVG_QSGD_TABLE_CAP, 64 MiB by default): written once and read by the
+        # fold, so ~2x these bytes of traffic ride on top of bytes_per_launch
+        cap = int(os.environ.get("FEDAVG_QSGD_TABLE_CAP", 64 << 20))
+        per_seg = N * 256 * 8
+        line["roofline"]["qsgd_table_bytes"] = min(T, max(1, cap // per_seg)) * per_seg
     print(json.dumps(line), flush=True)
     return 0
 

@@ -161,7 +161,8 @@ struct KArgs {
   int32_t zero_init;   // start every segment at the identity -0.0, ignore acc_in (shard partials)
   int32_t walk_back;   // the first walk_back tiles of the launch are walked last to first
                        // (fedavg_ctx::walk_reverse); 0 = natural order
-  const double* qtab;  // QSGD: [T][K][256] |product| tables of the call (qsgd_table_kernel)
+  const double* qtab;  // QSGD: [segments of the launch][K][256] |product| tables (qsgd_table_kernel)
+  int32_t qtab_seg0;   // QSGD: the segment of qtab's first table row
   // Multi-device peer exchange (multi_device.cpp): a zero-initialised partial launch whose tiles
   // [win_edge[j], win_edge[j+1]) store into win_dst[j] (device j's receive slot for this device,
   // accumulator coordinates) instead of acc; win_n = G windows, NULL = not windowed.
@@ -859,6 +860,7 @@ __global__ __launch_bounds__(kQsgdSlots) void qsgd_table_kernel(CallTables tab, 
   const int k = static_cast<int>(blockIdx.x);
   if (k >= to_const<int32_t>(tab.kseg)[seg]) return;
   const int64_t row = static_cast<int64_t>(seg) * K + k;
+  const int64_t trow = static_cast<int64_t>(blockIdx.y) * K + k;  // row of the launch's table block
   const void* rec = reinterpret_cast<const void*>(to_const<uint64_t>(tab.cptrs)[row]);
   const double norm = to_const<double>(rec)[0];
   const int level = to_const<int32_t>(rec)[2];
@@ -870,7 +872,7 @@ __global__ __launch_bounds__(kQsgdSlots) void qsgd_table_kernel(CallTables tab, 
   // LDS load instead of keeping norm and weight in SGPRs (the fold inserts every element's sign
   // itself, so entry 0's magnitude is all the fold takes from it)
   const bool flip = __builtin_signbit(norm) != __builtin_signbit(w);
-  qtab[row * kQsgdTable + s] = (s == 0 && flip) ? -p : p;
+  qtab[trow * kQsgdTable + s] = (s == 0 && flip) ? -p : p;
 }
 
 __device__ __forceinline__ void wait_vmcnt0() {
@@ -1018,7 +1020,7 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   };
   const int wave = __builtin_amdgcn_readfirstlane(li >> 6);
   const int lane = li & 63;
-  const double* const tabs = a.qtab + static_cast<int64_t>(seg) * a.K * kQsgdTable;
+  const double* const tabs = a.qtab + static_cast<int64_t>(seg - a.qtab_seg0) * a.K * kQsgdTable;
   auto issue = [&](GroupRegs& r, int buf, int k) {
     const int n = min(G, kseg - k);  // wave-uniform
 #pragma unroll
@@ -1648,6 +1650,8 @@ struct fedavg_ctx {
   // QSGD |product| tables of the current call ([T][K][256] fp64, qsgd_table_kernel)
   double* qtab = nullptr;
   size_t qtab_cap = 0;  // doubles
+  size_t qtab_cap_bytes = size_t(64) << 20;  // FEDAVG_QSGD_TABLE_CAP: table block per launch
+  size_t qtab_last_bytes = 0;                // table bytes of the last QSGD launch
   hipEvent_t aux_done = nullptr;  // the last upload out of aux_host finished
   bool aux_used = false;
 };
@@ -2082,6 +2086,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   a.zero_init = zero_init;
   a.walk_back = 0;
   a.qtab = nullptr;
+  a.qtab_seg0 = 0;
   int tb = 0, te = 0;
   if (split == 4) {
     // whole-layout launches only (tile ranges are defined on the SPLIT=1 table)
@@ -2169,8 +2174,15 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     return FEDAVG_OK;
   }
   if (is_qsgd(in_dtype)) {
-    // tables for the segments the launch's tiles touch, in a ctx buffer sized [T][K][256]
-    const size_t need = static_cast<size_t>(c->T) * static_cast<size_t>(a.K) * kQsgdTable;
+    // tables for the segments the launch's tiles touch ([segments][K][256] fp64, 2 KiB per
+    // (segment, client)); a launch whose tables would pass the cap (FEDAVG_QSGD_TABLE_CAP bytes,
+    // default 64 MiB: hundreds of clients over hundreds of tensors) runs as several launches over
+    // segment runs, each building its own tables into the same buffer
+    const size_t per_seg = static_cast<size_t>(a.K) * kQsgdTable;  // doubles
+    const size_t seg_first = static_cast<size_t>(c->tiles1[tb_split1].seg);
+    const size_t seg_span = static_cast<size_t>(c->tiles1[te_split1 - 1].seg) - seg_first + 1;
+    const size_t cap_segs = std::max<size_t>(1, c->qtab_cap_bytes / (per_seg * sizeof(double)));
+    const size_t need = std::min(seg_span, cap_segs) * per_seg;
     if (c->qtab_cap < need) {
       FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // an earlier launch may still read the old tables
       if (c->qtab) FEDAVG_HIP_TRY(hipFree(c->qtab));
@@ -2180,15 +2192,27 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
       c->qtab_cap = need;
     }
     a.qtab = c->qtab;
-    const int32_t seg0 = c->tiles1[tb_split1].seg;
-    const int32_t nseg = c->tiles1[te_split1 - 1].seg - seg0 + 1;
-    switch (out_kind) {
-      case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
-      case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
-      case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, a, st.aligned, s, e1, seg0, nseg); break;
-      default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
+    c->qtab_last_bytes = need * sizeof(double);
+    for (int32_t t0 = tb_split1; t0 < te_split1;) {
+      // tiles [t0, t1): whole segments' tiles while the run spans at most cap_segs segments
+      const int32_t seg0 = c->tiles1[t0].seg;
+      int32_t t1 = t0;
+      while (t1 < te_split1 && static_cast<size_t>(c->tiles1[t1].seg - seg0) < cap_segs) ++t1;
+      KArgs b = a;
+      b.tile_begin = t0;
+      b.num_tiles = t1 - t0;
+      b.qtab_seg0 = seg0;
+      const int32_t nseg = c->tiles1[t1 - 1].seg - seg0 + 1;
+      hipEvent_t eb = (t1 == te_split1) ? e1 : nullptr;  // the caller's event completes with the last
+      switch (out_kind) {
+        case OUT_ACC: err = launch_qsgd_out<OUT_ACC>(in_dtype, b, st.aligned, s, eb, seg0, nseg); break;
+        case OUT_F32: err = launch_qsgd_out<OUT_F32>(in_dtype, b, st.aligned, s, eb, seg0, nseg); break;
+        case OUT_F64: err = launch_qsgd_out<OUT_F64>(in_dtype, b, st.aligned, s, eb, seg0, nseg); break;
+        default: return fail(FEDAVG_ERR_INVALID, "bad out kind");
+      }
+      if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
+      t0 = t1;
     }
-    if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
     if (m1) {
       FEDAVG_HIP_TRY(hipEventRecord(m1, s));
       if (done_ev) *done_ev = m1;
@@ -2353,6 +2377,10 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
   c->wsum.assign(num_segments, -0.0);  // additive identity: the first weight is taken as is
   if (const char* e = std::getenv("FEDAVG_WIDE_MIN_CLIENTS")) c->wide_min_clients = std::atoi(e);
   if (const char* e = std::getenv("FEDAVG_WALK_ALTERNATE")) c->walk_alternate = std::atoi(e) != 0;
+  if (const char* e = std::getenv("FEDAVG_QSGD_TABLE_CAP")) {
+    const long long v = std::atoll(e);
+    if (v > 0) c->qtab_cap_bytes = static_cast<size_t>(v);
+  }
   c->valid.assign(num_segments, 0);
   build_tiles(c->seg_numel, kTile1, c->tiles1);
   build_tiles(c->seg_numel, kTile4, c->tiles4);

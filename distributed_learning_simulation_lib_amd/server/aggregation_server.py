@@ -55,8 +55,17 @@ class ModelCache:
         self._parameter = {k: v.detach().to(device="cpu", dtype=torch.float64) for k, v in parameter.items()}
 
     def get_parameter_diff(self, new_parameter: dict[str, torch.Tensor]) -> dict[str, torch.Tensor]:
+        """new - cached per name (model_cache.py:36-37); a device tensor keeps its device (the
+        cached fp64 copy goes to it: the subtraction is one elementwise torch op either way)."""
         assert self._parameter is not None
-        return {k: v - self._parameter[k] for k, v in new_parameter.items()}
+        return {k: v - self._parameter[k].to(v.device) for k, v in new_parameter.items()}
+
+    def add_parameter_diff(self, parameter_diff: dict[str, torch.Tensor]) -> None:
+        """cached += diff per cached name, the diff moved to the host first (model_cache.py:39-43:
+        ``v + tensor_to(parameter_diff[k], device="cpu")``; fp64 + the diff's dtype promotes as torch
+        does). The reference also re-points its storage file; this cache is in memory only."""
+        assert self._parameter is not None
+        self._parameter = {k: v + parameter_diff[k].to("cpu") for k, v in self._parameter.items()}
 
 
 class PipeServerEndpoint:

@@ -254,3 +254,35 @@ def test_random_quantised_rounds_bit_identical(hip_device, n, sizes, codec, leve
     got = algo.aggregate_worker_data().parameter
     for name, w in want.items():
         assert bits_equal(got[name].reshape(-1).cpu().numpy(), w.reshape(-1)), name
+
+
+@pytest.mark.parametrize("cap", [1, 3 * 2048 * 2, 1 << 30])
+def test_table_cap_splits_launches_bit_identically(hip_device, monkeypatch, cap):
+    # FEDAVG_QSGD_TABLE_CAP: a launch whose |p| tables would pass the cap runs over
+    # segment runs of at most cap / (clients x 2 KiB) segments (at least one), each building its own
+    # tables into one buffer; partial plans over tile ranges take the same path
+    monkeypatch.setenv("FEDAVG_QSGD_TABLE_CAP", str(cap))
+    numels = [4095, 4097, 33, 10_000, 1, 8192, 300]
+    rng = np.random.default_rng(7)
+    n_clients = 3
+    recs = make_round(rng, numels, n_clients, "float32")
+    weights = [float(rng.integers(1, 5000)) for _ in range(n_clients)]
+    want = oracle_result(recs, numels, "float32", weights)
+    layout = ModelLayout(names=tuple(f"t{i}" for i in range(len(numels))), shapes=tuple((n,) for n in numels))
+    ctx = FedAvgContext(layout, hip_device)
+    table = device_table(recs, numels, "float32", weights, hip_device)
+    outs = [torch.empty(n, dtype=torch.float64, device=hip_device) for n in numels]
+    ctx.aggregate(table, QSGD_F32, outs, torch.float64)
+    ctx.raise_on_nan([(table, QSGD_F32)])
+    for o, w in zip(outs, want):
+        assert bits_equal(o.cpu().numpy(), w)
+    # a ranged partial + finalize (the sharded path) under the same cap
+    W = sum(weights)
+    nt = ctx.num_tiles
+    for tb, te in ((0, nt // 3), (nt // 3, nt)):
+        ctx.partial(table, QSGD_F32, zero_init=True, tile_begin=tb, tile_end=te)
+    ctx.set_accumulated([W] * len(numels))
+    ctx.finalize_range(outs, torch.float64)
+    ctx.raise_on_nan()
+    for o, w in zip(outs, want):
+        assert bits_equal(o.cpu().numpy(), w)

@@ -158,6 +158,19 @@ def test_model_cache_copies_to_host_fp64():
     assert np.all(mc.parameter["x"].numpy() == 1.0)
 
 
+def test_model_cache_add_parameter_diff():
+    # model_cache.py:39-43: every cached name += the diff (moved to the host), fp64 kept
+    mc = ModelCache()
+    mc.cache_parameter({"x": torch.tensor([1.0, -2.0, 0.5]), "y": torch.zeros(2)})
+    diff = {"x": torch.tensor([0.25, 0.5, -0.5], dtype=torch.float32), "y": torch.tensor([1.0, 2.0], dtype=torch.float64)}
+    mc.add_parameter_diff(diff)
+    assert mc.parameter["x"].dtype == torch.float64 and mc.parameter["x"].tolist() == [1.25, -1.5, 0.0]
+    assert mc.parameter["y"].tolist() == [1.0, 2.0]
+    # get_parameter_diff undoes it
+    back = mc.get_parameter_diff({"x": torch.tensor([1.25, -1.5, 0.0], dtype=torch.float64), "y": torch.zeros(2, dtype=torch.float64)})
+    assert back["x"].tolist() == [0.0, 0.0, 0.0] and back["y"].tolist() == [-1.0, -2.0]
+
+
 def test_client_table_rejects_operands_the_kernel_would_misread():
     """A client tensor is read as a flat buffer of the layout's size: non-contiguous views are
     refused when added, wrong sizes / element sizes / devices before any launch (validate)."""

@@ -1766,6 +1766,7 @@ struct Staged {
 struct fedavg_plan {
   enum Kind { AGGREGATE = 0, PARTIAL = 1, FINALIZE = 2 };
   fedavg_ctx* ctx = nullptr;
+  int device = -1;  // the context's device (destroy must not read a context freed before it)
   Staged st;
   char* dev = nullptr;
   int32_t in_dtype = 0;
@@ -2876,6 +2877,7 @@ int32_t fedavg_plan_create(fedavg_ctx* c, const void* const* client_ptrs, int32_
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   auto* p = new fedavg_plan();
   p->ctx = c;
+  p->device = c->device;
   p->in_dtype = in_dtype;
   p->out_kind = ok;
   const BlobLayout L(c->T, K);
@@ -2915,6 +2917,7 @@ int32_t fedavg_plan_create_partial(fedavg_ctx* c, const void* const* client_ptrs
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   auto* p = new fedavg_plan();
   p->ctx = c;
+  p->device = c->device;
   p->kind = fedavg_plan::PARTIAL;
   p->in_dtype = K > 0 ? in_dtype : FEDAVG_F32;
   p->out_kind = OUT_ACC;
@@ -2946,6 +2949,7 @@ int32_t fedavg_plan_create_finalize(fedavg_ctx* c, const double* total_weights, 
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   auto* p = new fedavg_plan();
   p->ctx = c;
+  p->device = c->device;
   p->kind = fedavg_plan::FINALIZE;
   p->in_dtype = FEDAVG_F32;
   p->out_kind = ok;
@@ -3294,10 +3298,13 @@ int32_t fedavg_plan_run(fedavg_plan* p, void* stream) {
 
 int32_t fedavg_plan_destroy(fedavg_plan* p) {
   if (!p) return FEDAVG_OK;
-  if (p->ctx) (void)hipSetDevice(p->ctx->device);
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  if (p->device >= 0) (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();
   if (p->dev) (void)hipFree(p->dev);
   delete p;
+  if (prev >= 0) (void)hipSetDevice(prev);
   return FEDAVG_OK;
 }
 

@@ -274,8 +274,22 @@ int32_t root_finalize(fedavg_multi* m, const double* totals, void* const* outs, 
 
 extern "C" {
 
+// Every entry point switches devices (hipSetDevice per entry) and hands the caller's current
+// device back on return: the caller (torch's current device, a C program's hipSetDevice) must not
+// find its device changed by a call that only enqueued work.
+struct DeviceRestore {
+  int prev = -1;
+  DeviceRestore() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceRestore() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t num_devices, const int64_t* seg_numel,
                             int32_t num_segments, void* const* accumulators) {
+  DeviceRestore restore_device;
   if (!out) return invalid("null out");
   *out = nullptr;
   if (!devices || num_devices < 1 || num_devices > FEDAVG_MULTI_MAX_DEVICES)
@@ -348,6 +362,7 @@ int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t 
 }
 
 int32_t fedavg_multi_destroy(fedavg_multi* m) {
+  DeviceRestore restore_device;
   if (!m) return FEDAVG_OK;
   for (int32_t g = 0; g < m->G; ++g) {
     (void)hipSetDevice(m->devices[g]);
@@ -395,6 +410,7 @@ int32_t fedavg_multi_peer_access(const fedavg_multi* m) { return (m && m->peer_o
 int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const double* total_weights,
                            void* const* out_ptrs, int32_t out_dtype, int32_t root, const int32_t* tile_edges,
                            int32_t num_edges, int32_t exchange, void* const* streams) {
+  DeviceRestore restore_device;
   if (int32_t st = check_common(m, total_weights, out_ptrs, out_dtype, root)) return st;
   if (!partials) return invalid("null partial plan table");
   const int32_t n = m->num_tiles;
@@ -498,6 +514,7 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
 
 int32_t fedavg_multi_combine(fedavg_multi* m, const double* total_weights, void* const* out_ptrs, int32_t out_dtype,
                              int32_t root, int32_t exchange, void* const* streams) {
+  DeviceRestore restore_device;
   if (int32_t st = check_common(m, total_weights, out_ptrs, out_dtype, root)) return st;
   // which entries folded which segments (fed_avg_algorithm.py:55-62: a name the shard never saw)
   std::vector<std::vector<int32_t>> valid(m->G, std::vector<int32_t>(m->T, 0));
@@ -561,6 +578,7 @@ int32_t fedavg_multi_combine(fedavg_multi* m, const double* total_weights, void*
 }
 
 int32_t fedavg_multi_check(fedavg_multi* m, uint32_t* flags_out) {
+  DeviceRestore restore_device;
   if (!m) return invalid("null multi-device object");
   uint32_t f = 0;
   for (int32_t g = 0; g < m->G; ++g) {
@@ -577,6 +595,7 @@ int32_t fedavg_multi_check(fedavg_multi* m, uint32_t* flags_out) {
 }
 
 int32_t fedavg_multi_reset(fedavg_multi* m) {
+  DeviceRestore restore_device;
   if (!m) return invalid("null multi-device object");
   for (int32_t g = 0; g < m->G; ++g) {
     MULTI_HIP_TRY(hipSetDevice(m->devices[g]));

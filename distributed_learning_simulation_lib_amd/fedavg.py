@@ -15,6 +15,7 @@ arithmetic runs in the HIP kernels of ``csrc/fedavg_kernels.hip``; there is no C
 from __future__ import annotations
 
 import ctypes
+import weakref
 from collections.abc import Mapping, Sequence
 from dataclasses import dataclass
 from functools import cached_property
@@ -304,6 +305,7 @@ class FedAvgContext:
         lib: ctypes.CDLL | None = None,
     ) -> None:
         self._lib = lib if lib is not None else _native.load()
+        self._plans: weakref.WeakSet[AggregatePlan] = weakref.WeakSet()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         device = torch.device(device)
@@ -341,6 +343,7 @@ class FedAvgContext:
         ``multi_device.MultiDeviceContext``): same methods, but ``close`` leaves it alone."""
         self = cls.__new__(cls)
         self._lib = lib
+        self._plans = weakref.WeakSet()
         self.device = device
         self.layout = layout
         self.accumulator = accumulator
@@ -363,6 +366,8 @@ class FedAvgContext:
 
     # -- lifecycle -------------------------------------------------------------------
     def close(self) -> None:
+        for plan in list(getattr(self, "_plans", ())):
+            plan.close()  # before the native context goes: a plan reads it
         if getattr(self, "_borrowed", False):
             self._h = ctypes.c_void_p()  # the owner destroys it
             return
@@ -683,6 +688,7 @@ class AggregatePlan:
         self.ctx = ctx
         self._h = handle
         self._keep = keep
+        ctx._plans.add(self)  # closed with the context (a native plan points at its context)
 
     def run(self) -> None:
         _native.check(self.ctx._lib.fedavg_plan_run(self._h, self.ctx.stream))

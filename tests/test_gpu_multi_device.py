@@ -116,6 +116,28 @@ def test_peer_round_with_an_entry_without_clients(hip_device):
         m.close()
 
 
+def test_plans_outliving_the_multi_context_leave_no_hip_error(hip_device):
+    """Closing the multi-device object closes the plans of its entries first (a native plan reads
+    its context); a plan dropped afterwards and the next torch launch see no sticky HIP error, and
+    the caller's current device is the one it set."""
+    import gc
+
+    dev_before = torch.cuda.current_device()
+    m = MultiDeviceContext(LAYOUT, [0, 0])
+    t = ClientTable(LAYOUT.num_segments)
+    t.add_client([x.to(hip_device) for x in _clients(1, torch.float32, 1)[0]], [3.0] * LAYOUT.num_segments)
+    partials = m.plan_partials([t, None], torch.float32)
+    outs = [torch.empty(s, dtype=torch.float32, device=hip_device) for s in LAYOUT.numels]
+    m.round(partials, [3.0] * LAYOUT.num_segments, outs, torch.float32)
+    m.raise_on_nan()
+    m.close()
+    del partials
+    gc.collect()
+    assert torch.cuda.current_device() == dev_before
+    assert float(torch.ones(8, device=hip_device).sum().item()) == 8.0
+    torch.cuda.synchronize(hip_device)
+
+
 def test_peer_round_nan_input_names_the_client(hip_device):
     world, n = 3, 6
     clients = _clients(n, torch.float32, 5)

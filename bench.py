@@ -852,7 +852,8 @@ def main_plugin(args: argparse.Namespace) -> int:
     buckets, views = make_clients(layout, 0, N, device, in_dtype)
     params = [{n: v.view(s) for n, s, v in zip(layout.names, layout.shapes, row)} for row in views]
     weights = dataset_size_weights(N)
-    algo = FedAVGAlgorithm(device=device, wave_size=args.wave if args.wave > 0 else None, result_dtype=out_dtype)
+    algo = FedAVGAlgorithm(device=device, wave_size=args.wave if args.wave > 0 else None, result_dtype=out_dtype,
+                           wave_min=args.wave_min if args.wave_min >= 0 else None)
     wave = min(algo.wave_size, N)  # the plugin's own default unless --wave is given
 
     # --workload gradient: GradientWorker._process_gradient's message every step (gradient_worker.py:
@@ -891,6 +892,8 @@ def main_plugin(args: argparse.Namespace) -> int:
     in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
     job_bytes = N * P * in_b + P * out_b
     n_waves = -(-N // wave)
+    if algo.wave_min and launches and not args.no_kernel_events:
+        n_waves = max(1, round(launches / args.steps))  # early waves: the launches that ran
     launch_bytes = job_bytes + (n_waves - 1) * P * 16  # + the fp64 accumulator round trips between waves
     step_s = elapsed / args.steps
     kstep_s = kernel_ms * 1e-3 / args.steps
@@ -916,9 +919,11 @@ def main_plugin(args: argparse.Namespace) -> int:
         "scaling": "replicas only", "vs_baseline": None, "dtype": "f64", "GBps": gbps,
         "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
         "config": {"workload": (f"{'gradient' if in_round else 'plugin'}_fedavg_{args.layout}_{short}_{N}_clients"
-                                + (f"_waves_of_{wave}" if n_waves > 1 else "")),
+                                + (f"_waves_of_{wave}" if n_waves > 1 and not algo.wave_min else "")
+                                + (f"_early_waves_from_{algo.wave_min}" if algo.wave_min else "")),
                    "clients": N, "params_per_client": P, "tensors_per_client": T, "in_dtype": args.in_dtype,
-                   "out_dtype": args.out_dtype, "clients_per_launch": wave, "in_round": in_round,
+                   "out_dtype": args.out_dtype, "clients_per_launch": wave, "wave_min": algo.wave_min,
+                   "waves_per_round": round(launches / args.steps, 2) if launches else None, "in_round": in_round,
                    "host_us_per_update": round(host_s[0] / (args.steps * N) * 1e6, 2),
                    "process_worker_data_ms_per_round": round(host_s[0] / args.steps * 1e3, 4),
                    # what a round costs beyond its kernels: staging, launch, NaN readback, result dict
@@ -1290,6 +1295,9 @@ def main() -> int:
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling instead: --clients-per-gpu clients on every rank")
     ap.add_argument("--wave", type=int, default=0, help="clients per launch (streaming waves); 0 = all")
+    ap.add_argument("--wave-min", type=int, default=-1,
+                    help="plugin early waves: fold >= this many staged clients whenever the GPU is idle "
+                         "(0 = full waves only; -1 = the plugin's default)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="tile chunks of the sharded reduce (0 = auto: 4 when world > 1 — "
                          "the RCCL reduce of chunk c overlaps the partial of chunk c+1, DESIGN.md §5)")

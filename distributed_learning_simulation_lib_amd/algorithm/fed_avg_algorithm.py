@@ -76,7 +76,7 @@ _HOST_RECORD_PTRS = os.environ.get("FEDAVG_QSGD_HOST_PTRS", "1") != "0"
 # layout, per-name totals, flags — is one for the whole round)
 _LANE_ATTRS = ("_device", "_FedAVGAlgorithm__table", "_FedAVGAlgorithm__table_dtype",
                "_FedAVGAlgorithm__table_delta", "_FedAVGAlgorithm__ingest", "_FedAVGAlgorithm__fast",
-               "_FedAVGAlgorithm__base")
+               "_FedAVGAlgorithm__base", "_FedAVGAlgorithm__wave_event")
 
 
 def _is_elementwise(weight: Any, parameter: Any) -> bool:
@@ -116,6 +116,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         eager_nan_check: bool | None = None,
         devices: Sequence[int | str | torch.device] | None = None,
         exchange: str = "peer",
+        wave_min: int | None = None,
     ) -> None:
         super().__init__()
         self.accumulate: bool = True
@@ -126,6 +127,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         # fp64 accumulator round trip per extra wave
         self.wave_size = int(wave_size or os.environ.get("FEDAVG_WAVE_SIZE", 32))
         assert self.wave_size >= 1
+        # early waves: a wave of at least ``wave_min`` staged clients is also folded when the next
+        # update arrives while the GPU has finished every wave so far (0 = only full waves), so the
+        # fold starts after the first few arrivals instead of after ``wave_size`` of them
+        self.wave_min = int(os.environ.get("FEDAVG_WAVE_MIN", 0) if wave_min is None else wave_min)
+        assert self.wave_min >= 0
+        self.__wave_event: torch.cuda.Event | None = None  # recorded after each flushed wave
         self.result_dtype = result_dtype
         self.result_device = torch.device(result_device) if result_device is not None else None
         self.split_policy = split_policy
@@ -438,7 +445,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             if fast is None:
                 return False
         _, index, shapes, dev_idx = fast
-        if self.__table is not None and self.__table.num_clients >= self.wave_size:
+        if self.__table is not None and self._wave_due(self.__table.num_clients):
             self._flush()  # a full wave is folded when the next update arrives (see _stage_client)
         table = self.__table
         fresh = table is None
@@ -713,7 +720,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         # wave then always reaches aggregate_worker_data unfolded and is folded and divided in one
         # launch (fedavg_aggregate) instead of an accumulate launch plus a finalize pass.
         if self.__table is not None and (self.__table_dtype != dt or self.__table_delta != delta
-                                         or self.__table.num_clients >= self.wave_size):
+                                         or self._wave_due(self.__table.num_clients)):
             self._flush()
         if self.__table is None:
             self.__table = self._new_table(dev_idx)
@@ -822,6 +829,16 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         assert self.__native_layout is not None
         return [self.__tot_fp32.get(n, False) for n in self.__native_layout.names]
 
+    def _wave_due(self, staged: int) -> bool:
+        """Fold the staged wave before the arriving update joins it: it is full, or it holds at
+        least ``wave_min`` clients and the GPU has finished every wave flushed so far."""
+        if staged >= self.wave_size:
+            return True
+        if not self.wave_min or staged < self.wave_min:
+            return False
+        ev = self.__wave_event
+        return ev is None or ev.query()
+
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""
         if self.__table is None or self.__table.num_clients == 0:
@@ -836,6 +853,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             ctx.accumulate_delta(table, dt, self._delta_base())
         else:
             ctx.accumulate(table, dt)
+        if self.wave_min:
+            if self.__wave_event is None:
+                self.__wave_event = torch.cuda.Event()
+            self.__wave_event.record(torch.cuda.current_stream(self.device))
 
     # ---- end of round (fed_avg_algorithm.py:76-113) ------------------------------------
     def _aggregate_parameter(self, chosen_worker_ids: set[int] | None = None) -> ModelParameter:

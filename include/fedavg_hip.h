@@ -484,6 +484,9 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
  *       of every context's NaN flags like fedavg_check; fedavg_multi_reset clears them.
  * Results: each device's fold is the exact arrival-order chain of its clients; PEER sums the
  * partials in device order (bit-identical to that host composition), REDUCE in RCCL's order.
+ * Every call returns with the caller's current device (hipGetDevice) unchanged. Destroy the
+ * plans made on the entries' contexts before (or after) fedavg_multi_destroy: a plan keeps its
+ * device, not its context, for its own destroy, but must not be run once the object is gone.
  * ===================================================================================== */
 #define FEDAVG_EXCHANGE_PEER 2
 #define FEDAVG_MULTI_MAX_DEVICES 16

@@ -1,5 +1,5 @@
 """Where a plugin round's time goes beyond its kernel (GPU box): 64 device-resident ResNet-18 fp32
-updates through FedAVGAlgorithm (one wave), wall-clock marks around the pieces of
+updates through FedAVGAlgorithm (argv: clients, wave size, wave_min), wall-clock marks around the pieces of
 aggregate_worker_data (FedAvgContext.aggregate = staging + enqueue, raise_on_nan = the sync + NaN
 flags, the rest = result views / message), with the kernel's own duration from the library's
 profiling events. Prints one JSON line (means over R rounds, microseconds)."""
@@ -20,6 +20,8 @@ from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMe
 from distributed_learning_simulation_lib_amd.fedavg import FedAvgContext  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+WAVE = int(sys.argv[2]) if len(sys.argv) > 2 else K
+WAVE_MIN = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 R = 40
 dev = torch.device("cuda", 0)
 layout = resnet18_layout()
@@ -58,7 +60,7 @@ def reset(self, *a, **k):
 
 
 FedAvgContext.aggregate, FedAvgContext.raise_on_nan, FedAvgContext.reset = agg, nan, reset
-algo = FedAVGAlgorithm(device=dev, wave_size=K)
+algo = FedAVGAlgorithm(device=dev, wave_size=WAVE, wave_min=WAVE_MIN)
 msgs = lambda: [ParameterMessage(parameter=dict(p), aggregation_weight=x) for p, x in zip(params, w)]  # noqa: E731
 for _ in range(3):
     for i, m in enumerate(msgs()):
@@ -107,6 +109,7 @@ out = {k + "_us": round(v / R * 1e6, 1) for k, v in acc.items()}
 out["kernel_us"] = round(kernel_ms * 1e3 / max(launches, 1), 1)
 out["launches_per_round"] = launches / R
 out["clients"] = K
+out["wave_size"], out["wave_min"] = WAVE, WAVE_MIN
 out["reset_us_per_call"] = round(reset_acc[0] / max(reset_acc[1], 1) * 1e6, 1)
 out["reset_calls_per_round"] = reset_acc[1] / (R + 3)
 print(json.dumps(out))

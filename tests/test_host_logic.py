@@ -188,3 +188,26 @@ def test_client_table_rejects_operands_the_kernel_would_misread():
         t.validate([16, 3], 2, -1, "dtype")
     with pytest.raises(ValueError, match="on device -1"):
         t.validate([16, 3], 4, 0, "device")
+
+
+def test_early_wave_policy():
+    """wave_min: a partial wave of >= wave_min staged clients is folded at the next arrival only
+    while the GPU has finished the waves flushed so far; a full wave always is; 0 disables it."""
+    from distributed_learning_simulation_lib_amd import FedAVGAlgorithm
+
+    class Ev:
+        def __init__(self, done: bool) -> None:
+            self.done = done
+
+        def query(self) -> bool:
+            return self.done
+
+    a = FedAVGAlgorithm(device="cpu", wave_size=8, wave_min=3)
+    assert a._wave_due(8) and not a._wave_due(2)
+    assert a._wave_due(3)  # nothing flushed yet: the GPU is idle
+    a._FedAVGAlgorithm__wave_event = Ev(False)
+    assert not a._wave_due(5) and a._wave_due(8)
+    a._FedAVGAlgorithm__wave_event = Ev(True)
+    assert a._wave_due(3) and not a._wave_due(2)
+    b = FedAVGAlgorithm(device="cpu", wave_size=8, wave_min=0)
+    assert not b._wave_due(7) and b._wave_due(8)

@@ -1596,6 +1596,9 @@ def main() -> int:
     workload = workload_name(args, world, n_total, n_waves, wave)
     predicted = None if world < 2 else model.round_ms(
         world, P, n_total, in_b, out_b, chunk_edges(ctx.num_tiles, args.chunks, chunk_shape), exchange)
+    # the single-process peer exchange (--procs 1) at its best schedule, for comparison
+    peer_cand, peer_pred = (None, None) if world < 2 else model.best(
+        world, P, n_total, in_b, out_b, ctx.num_tiles, candidates=exchange_candidates(exchanges=("peer",)))
     if args.layout == "resnet18" and not args.weak and n_total == 64 and world == 1:
         baseline_config = "BASELINE.json configs[1]"
     elif args.layout == "resnet18" and not args.weak and n_total == 256:
@@ -1643,6 +1646,8 @@ def main() -> int:
                 # rate x assumed RCCL efficiency): its fold / exposed terms beside the measured ones
                 "predicted_speedup": None if predicted is None else predicted["speedup"],
                 "predicted": predicted,
+                "peer_mode_predicted_speedup": None if peer_pred is None else peer_pred["speedup"],
+                "peer_mode_predicted": None if peer_pred is None else dict(peer_pred, schedule=list(peer_cand)),
             },
             "baseline_config": baseline_config,
             **({"rehearsal": "all ranks on cuda:0 over gloo: a code-path check, not an N-GPU measurement"}

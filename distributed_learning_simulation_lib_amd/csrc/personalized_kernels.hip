@@ -356,6 +356,17 @@ struct Glds<float> {
     x[2] = v.z;
     x[3] = v.w;
   }
+  // the split fold reads a slice one client ahead and widens it only after its wait
+  using RawT = f32x4;
+  __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
+    return *reinterpret_cast<const f32x4*>(slot + lane * 16);
+  }
+  __device__ __forceinline__ static void expand(RawT v, double* x) {
+    x[0] = v.x;
+    x[1] = v.y;
+    x[2] = v.z;
+    x[3] = v.w;
+  }
 };
 template <>
 struct Glds<double> {
@@ -376,15 +387,109 @@ struct Glds<double> {
     x[2] = hi.x;
     x[3] = hi.y;
   }
+  using RawT = f64x2x2;
+  __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
+    return RawT{*reinterpret_cast<const f64x2*>(slot + lane * 16), *reinterpret_cast<const f64x2*>(slot + 1024 + lane * 16)};
+  }
+  __device__ __forceinline__ static void expand(RawT v, double* x) {
+    x[0] = v.lo.x;
+    x[1] = v.lo.y;
+    x[2] = v.hi.x;
+    x[3] = v.hi.y;
+  }
 };
 template <typename T>
 constexpr bool kHasGlds = std::is_same<T, float>::value || std::is_same<T, double>::value;
 
 // The main loop on the LDS ring: acc[v][j] += x_k[v] * w_kj for every client k of the
 // (padded) list, in order. Requires a whole chunk and 16-B aligned client pointers.
+#ifndef PERS_SPLIT
+#define PERS_SPLIT 1
+#endif
+// The ring fold with the weight loads hidden under the FMAs. Scalar loads complete out of order,
+// so a wave can only wait for all of them at once (lgkmcnt(0)): loading a client's 16 weights and
+// then waiting exposes the scalar-load latency once per client. Here the receivers are split in
+// halves: while the low half's 32 FMAs of client c run, the high half's weights of c load; while
+// the high half's FMAs run, the low half's weights and the x slice of client c + 1 load. Each wait
+// then comes after 32 FMAs, with the same 32 weight SGPRs live as before (two halves of 8).
+template <typename T, int FOLD>
+__device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int lane, int64_t sb, kp<uint64_t> ptrs,
+                                                kp<double> wt, char* ring, double (&acc)[kVE][kJB]) {
+  using G = Glds<T>;
+  constexpr int H = kJB / 2;
+  const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
+  const int waves = a.waves;
+  const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
+  const int nst = a.Npad / kSC;
+  auto issue = [&](int st) {
+    char* stage = ring + (st % kRS) * (kSC * G::kSlice);
+    for (int i = 0; i < per; ++i) {
+      const int c = wave + i * waves;
+      const uint64_t p = ptrs[st * kSC + c];
+      G::issue(p ? p + sb : zeros, lane, stage + c * G::kSlice);
+    }
+  };
+  // stage st is usable once this wave's DMAs of it landed and the barrier saw every wave's
+  auto enter = [&](int st) {
+    if (st + kD < nst) issue(st + kD);
+    const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;
+    wait_vmcnt(ahead * per * G::kIPC);
+    __builtin_amdgcn_s_barrier();
+  };
+  auto slot = [&](int k) { return ring + ((k / kSC) % kRS) * (kSC * G::kSlice) + (k % kSC) * G::kSlice; };
+  for (int st = 0; st < kD && st < nst; ++st) issue(st);
+  enter(0);
+  typename G::RawT xr = G::read_raw(slot(0), lane);
+  double wlo[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) wlo[j] = wt[j];
+  const int n = a.Npad;
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) {
+    const kp<double> wk = wt + static_cast<int64_t>(k) * a.wstride;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the x slice and the low weights of k
+    __builtin_amdgcn_sched_barrier(0);
+    double whi[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) whi[j] = wk[H + j];
+    __builtin_amdgcn_sched_barrier(0);
+    double x[kVE];
+    G::expand(xr, x);
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+#pragma unroll
+      for (int v = 0; v < kVE; ++v) {
+        acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wlo[j]);
+        // pins the low half's FMAs here: without it they are sunk past the stage branch below,
+        // behind the wait they are meant to hide
+        asm volatile("" : "+v"(acc[v][j]));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the high weights of k
+    __builtin_amdgcn_sched_barrier(0);
+    // next client (the last one re-reads itself): its stage may need entering first
+    const int kn = k + 1 < n ? k + 1 : k;
+    if (kn != k && kn % kSC == 0) enter(kn / kSC);
+    xr = G::read_raw(slot(kn), lane);
+    const kp<double> wn = wt + static_cast<int64_t>(kn) * a.wstride;
+#pragma unroll
+    for (int j = 0; j < H; ++j) wlo[j] = wn[j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+#pragma unroll
+      for (int v = 0; v < kVE; ++v) acc[v][H + j] = pfold<FOLD>(acc[v][H + j], x[v], whi[j]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <typename T, int FOLD>
 __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, int64_t sb, kp<uint64_t> ptrs,
                                           kp<double> wt, char* ring, double (&acc)[kVE][kJB]) {
+#if PERS_SPLIT
+  fold_ring_split<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
+  return;
+#endif
   using G = Glds<T>;
   const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
   const int waves = a.waves;
@@ -445,6 +550,59 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 
   if constexpr (RING) {
     fold_ring<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
+  } else if constexpr (PERS_SPLIT != 0) {
+    // the register pipeline (client slices loaded one group ahead) with the split weight loads
+    // of fold_ring_split: each lgkmcnt(0) wait comes after half a client's folds
+    constexpr int H = kJB / 2;
+    RT nxt[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[u], sb, zeros), e, count);
+    double wlo[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) wlo[j] = wt[j];
+    const int n = a.Npad;
+    for (int k = 0; k < n; k += kU) {
+      RT cur[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) cur[u] = nxt[u];
+      const int kn = (k + kU < n) ? k + kU : k;  // the last group re-loads itself (L2 hits)
+#pragma unroll
+      for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[kn + u], sb, zeros), e, count);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int kk = k + u;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the low weights of kk
+        __builtin_amdgcn_sched_barrier(0);
+        const kp<double> wk = wt + static_cast<int64_t>(kk) * a.wstride;
+        double whi[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) whi[j] = wk[H + j];
+        __builtin_amdgcn_sched_barrier(0);
+        double x[kVE];
+        R::expand(cur[u], x);
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+#pragma unroll
+          for (int v = 0; v < kVE; ++v) {
+            acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wlo[j]);
+            asm volatile("" : "+v"(acc[v][j]));
+          }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the high weights of kk
+        __builtin_amdgcn_sched_barrier(0);
+        const int k1 = kk + 1 < n ? kk + 1 : kk;
+        const kp<double> w1 = wt + static_cast<int64_t>(k1) * a.wstride;
+#pragma unroll
+        for (int j = 0; j < H; ++j) wlo[j] = w1[j];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+#pragma unroll
+          for (int v = 0; v < kVE; ++v) acc[v][H + j] = pfold<FOLD>(acc[v][H + j], x[v], whi[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   } else {
   RT nxt[kU];
 #pragma unroll

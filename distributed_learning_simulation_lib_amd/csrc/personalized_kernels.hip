@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <string>
@@ -229,6 +230,14 @@ static_assert(kVE == 4, "the Raw loaders move 4 elements per lane");
 
 enum PFold : int { PF_MULADD = 0, PF_FMA = 1 };
 
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 template <int FOLD>
 __device__ __forceinline__ double pfold(double acc, double x, double w) {
   if constexpr (FOLD == PF_FMA) {
@@ -236,6 +245,51 @@ __device__ __forceinline__ double pfold(double acc, double x, double w) {
   } else {
     const double p = x * w;  // tmp = x.to(float64) * w   (fed_avg_algorithm.py:54)
     return acc + p;          // acc += tmp                 (:58)
+  }
+}
+
+#ifndef PERS_MA_GROUP  // receivers whose products issue before their sums (separately rounded fold)
+#define PERS_MA_GROUP 1
+#endif
+// acc[v][J0 + j] (+)= x[v] * w[j] for the H receivers of one half. The separately rounded fold
+// issues each receiver's 4 products before their 4 sums (the dependent add right behind its
+// multiply stalls the wave); PIN keeps every sum in place (see fold_ring_split).
+template <int FOLD, int J0, int H, bool PIN, bool BATCH = true>
+__device__ __forceinline__ void fold_half(double (&acc)[kVE][kJB], const double* x, const double* w) {
+  if constexpr (FOLD == PF_MULADD && !BATCH) {
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+#pragma unroll
+      for (int v = 0; v < kVE; ++v) {
+        acc[v][J0 + j] = pfold<FOLD>(acc[v][J0 + j], x[v], w[j]);
+        if constexpr (PIN) asm volatile("" : "+v"(acc[v][J0 + j]));
+      }
+  } else if constexpr (FOLD == PF_FMA) {
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+#pragma unroll
+      for (int v = 0; v < kVE; ++v) {
+        acc[v][J0 + j] = __builtin_fma(x[v], w[j], acc[v][J0 + j]);
+        if constexpr (PIN) asm volatile("" : "+v"(acc[v][J0 + j]));
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < H; j += PERS_MA_GROUP) {
+      double p[PERS_MA_GROUP][kVE];
+#pragma unroll
+      for (int jj = 0; jj < PERS_MA_GROUP; ++jj)
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) p[jj][v] = x[v] * w[j + jj];  // tmp = x.to(float64) * w (:54)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jj = 0; jj < PERS_MA_GROUP; ++jj)
+#pragma unroll
+        for (int v = 0; v < kVE; ++v) {
+          acc[v][J0 + j + jj] = acc[v][J0 + j + jj] + p[jj][v];  // acc += tmp (:58)
+          if constexpr (PIN) asm volatile("" : "+v"(acc[v][J0 + j + jj]));
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
@@ -455,15 +509,7 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
     __builtin_amdgcn_sched_barrier(0);
     double x[kVE];
     G::expand(xr, x);
-#pragma unroll
-    for (int j = 0; j < H; ++j)
-#pragma unroll
-      for (int v = 0; v < kVE; ++v) {
-        acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wlo[j]);
-        // pins the low half's FMAs here: without it they are sunk past the stage branch below,
-        // behind the wait they are meant to hide
-        asm volatile("" : "+v"(acc[v][j]));
-      }
+    fold_half<FOLD, 0, H, true>(acc, x, wlo);  // pinned ahead of the stage branch below
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the high weights of k
     __builtin_amdgcn_sched_barrier(0);
@@ -475,10 +521,7 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
 #pragma unroll
     for (int j = 0; j < H; ++j) wlo[j] = wn[j];
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < H; ++j)
-#pragma unroll
-      for (int v = 0; v < kVE; ++v) acc[v][H + j] = pfold<FOLD>(acc[v][H + j], x[v], whi[j]);
+    fold_half<FOLD, H, H, false>(acc, x, whi);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -581,13 +624,8 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
         __builtin_amdgcn_sched_barrier(0);
         double x[kVE];
         R::expand(cur[u], x);
-#pragma unroll
-        for (int j = 0; j < H; ++j)
-#pragma unroll
-          for (int v = 0; v < kVE; ++v) {
-            acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wlo[j]);
-            asm volatile("" : "+v"(acc[v][j]));
-          }
+        // (fp64 inputs keep the plain order: their raw slices leave no registers for the products)
+        fold_half<FOLD, 0, H, true, !std::is_same<T, double>::value>(acc, x, wlo);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the high weights of kk
         __builtin_amdgcn_sched_barrier(0);
@@ -596,10 +634,7 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 #pragma unroll
         for (int j = 0; j < H; ++j) wlo[j] = w1[j];
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < H; ++j)
-#pragma unroll
-          for (int v = 0; v < kVE; ++v) acc[v][H + j] = pfold<FOLD>(acc[v][H + j], x[v], whi[j]);
+        fold_half<FOLD, H, H, false, !std::is_same<T, double>::value>(acc, x, whi);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -738,7 +773,8 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 }
 
 template <typename T, int FOLD>
-__global__ __launch_bounds__(64 * kMaxWaves) void personalized_kernel(PArgs a) {
+// three waves per SIMD (<= 168 VGPRs): the fold hides its load latency across waves
+__global__ __launch_bounds__(64 * kMaxWaves) __attribute__((amdgpu_waves_per_eu(3))) void personalized_kernel(PArgs a) {
   // dynamic LDS: the centralized chain (64 x kVE doubles), then the client ring (fp32 / fp64)
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* chain = smem;
@@ -750,7 +786,7 @@ __global__ __launch_bounds__(64 * kMaxWaves) void personalized_kernel(PArgs a) {
   const int count = cd[1];
   const int64_t start = ((kp<int64_t>)(a.chunks + blockIdx.x))[1];
   if (count == kChunk && a.aligned) {
-    if constexpr (kHasGlds<T>) {
+    if constexpr (kHasGlds<T> && FOLD == PF_FMA) {  // the host enables the ring for the fused fold only
       if (a.ring) {
         pers_body<T, FOLD, true, true>(a, wave, lane, seg, count, start, chain, ring);
         return;
@@ -831,6 +867,7 @@ struct fedavg_pers {
   hipEvent_t blob_done = nullptr;
   bool blob_used = false;
   bool allow_fma = true;
+  bool ring = true;  // FEDAVG_PERS_RING=0: the fused fold of whole chunks takes the register pipeline too (A/B)
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
 };
@@ -891,6 +928,7 @@ int32_t fedavg_pers_create(fedavg_pers** out, int32_t device, const int64_t* seg
   fedavg_pers* p = new fedavg_pers();
   p->device = device;
   p->T = num_segments;
+  if (const char* e = std::getenv("FEDAVG_PERS_RING")) p->ring = std::strcmp(e, "0") != 0;
   p->seg_numel.assign(seg_numel, seg_numel + num_segments);
   p->seg_off.resize(num_segments);
   for (int t = 0; t < num_segments; ++t) {
@@ -1143,7 +1181,7 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
     // the LDS ring (whole aligned fp32 / fp64 chunks) for the fused fold: measured 3.08 -> 2.85 ms
     // (64 x 64 ResNet-18); the mul + add fold is VALU-bound and ~3 % faster on the register
     // pipeline, which every other case keeps
-    a.ring = fold == PF_FMA && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
+    a.ring = p->ring && fold == PF_FMA && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
     const size_t slice = static_cast<size_t>(kChunk) * (in_dtype == FEDAVG_F64 ? 8 : 4);
     const size_t lds = sizeof(double) * 64 * kVE +
                        (a.ring ? kRS * kSC * slice : 0);

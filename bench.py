@@ -776,7 +776,9 @@ def main_qsgd(args: argparse.Namespace) -> int:
     achieved = job_bytes / per_launch_s / 1e9
     probe = None if args.no_probe else hbm_probes(device)
     traffic, traffic_src = None, None
-    tfile = REPO / "profiles" / f"r03_traffic_{'nnadq' if nnadq else 'qsgd'}.json"  # PMC pass of this line
+    # the newest PMC pass of this line's kernel (QSGD: round 4's XCD-contiguous placement)
+    cands = sorted((REPO / "profiles").glob(f"r[0-9][0-9]_traffic_{'nnadq' if nnadq else 'qsgd'}.json"))
+    tfile = cands[-1] if cands else REPO / "profiles" / "missing.json"
     if tfile.exists() and N == 64 and args.layout == "resnet18" and out_dtype == torch.float32:
         traffic = float(json.loads(tfile.read_text())["hbm_traffic_bytes_per_step"])
         traffic_src = f"profiles/{tfile.name}"

@@ -1123,22 +1123,15 @@ __device__ __forceinline__ void qsgd_tile_body(const KArgs& a, const TileDesc& t
   record_tile_finish<OUT, FULL, VEC, AE>(a, td, acc_base, e0, acc);
 }
 
-#ifndef FEDAVG_QSGD_XCD_SWIZZLE
-#define FEDAVG_QSGD_XCD_SWIZZLE 1
-#endif
 // Block b runs on XCD b % 8 (round-robin dispatch); the launch's tiles are segment-ordered, so
 // giving XCD x the x-th contiguous eighth of them (the bijective form for any grid size) keeps each
-// segment's |p| tables in one or two XCD L2s instead of all eight. Placement affects speed only.
+// segment's |p| tables in one or two XCD L2s instead of all eight: 953 -> 882 MB fetched per
+// 64 x ResNet-18 launch (profiles/r04_traffic_qsgd.json). Placement affects speed only.
 __device__ __forceinline__ int xcd_contiguous(int b, int n) {
-#if FEDAVG_QSGD_XCD_SWIZZLE
   constexpr int kX = 8;
   const int q = n / kX, r = n % kX;
   const int x = b % kX, k = b / kX;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-#else
-  (void)n;
-  return b;
-#endif
 }
 
 template <int OUT, typename DQ, bool VEC>

@@ -457,8 +457,8 @@ constexpr bool kHasGlds = std::is_same<T, float>::value || std::is_same<T, doubl
 
 // The main loop on the LDS ring: acc[v][j] += x_k[v] * w_kj for every client k of the
 // (padded) list, in order. Requires a whole chunk and 16-B aligned client pointers.
-#ifndef PERS_SPLIT
-#define PERS_SPLIT 1
+#ifndef PERS_RING_SPLIT  // ring loop A/B: 0 = one wait per client, 1 = halves, 2 = next client's weights ahead
+#define PERS_RING_SPLIT 1
 #endif
 // The ring fold with the weight loads hidden under the FMAs. Scalar loads complete out of order,
 // so a wave can only wait for all of them at once (lgkmcnt(0)): loading a client's 16 weights and
@@ -526,11 +526,66 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
   }
 }
 
+// PERS_RING_SPLIT == 2: client k + 1's weights (both halves) and x slice load while client k's
+// 64 folds run (64 weight SGPRs live instead of 32).
+template <typename T, int FOLD>
+__device__ __forceinline__ void fold_ring_ahead(const PArgs& a, int wave, int lane, int64_t sb, kp<uint64_t> ptrs,
+                                                kp<double> wt, char* ring, double (&acc)[kVE][kJB]) {
+  using G = Glds<T>;
+  const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
+  const int waves = a.waves;
+  const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
+  const int nst = a.Npad / kSC;
+  auto issue = [&](int st) {
+    char* stage = ring + (st % kRS) * (kSC * G::kSlice);
+    for (int i = 0; i < per; ++i) {
+      const int c = wave + i * waves;
+      const uint64_t p = ptrs[st * kSC + c];
+      G::issue(p ? p + sb : zeros, lane, stage + c * G::kSlice);
+    }
+  };
+  auto enter = [&](int st) {
+    if (st + kD < nst) issue(st + kD);
+    const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;
+    wait_vmcnt(ahead * per * G::kIPC);
+    __builtin_amdgcn_s_barrier();
+  };
+  auto slot = [&](int k) { return ring + ((k / kSC) % kRS) * (kSC * G::kSlice) + (k % kSC) * G::kSlice; };
+  for (int st = 0; st < kD && st < nst; ++st) issue(st);
+  enter(0);
+  typename G::RawT xr = G::read_raw(slot(0), lane);
+  double w[kJB];
+#pragma unroll
+  for (int j = 0; j < kJB; ++j) w[j] = wt[j];
+  const int n = a.Npad;
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): x slice and weights of k
+    __builtin_amdgcn_sched_barrier(0);
+    double x[kVE], wc[kJB];
+    G::expand(xr, x);
+#pragma unroll
+    for (int j = 0; j < kJB; ++j) wc[j] = w[j];
+    const int kn = k + 1 < n ? k + 1 : k;
+    if (kn != k && kn % kSC == 0) enter(kn / kSC);
+    xr = G::read_raw(slot(kn), lane);
+    const kp<double> wn = wt + static_cast<int64_t>(kn) * a.wstride;
+#pragma unroll
+    for (int j = 0; j < kJB; ++j) w[j] = wn[j];
+    __builtin_amdgcn_sched_barrier(0);
+    fold_half<FOLD, 0, kJB, false>(acc, x, wc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <typename T, int FOLD>
 __device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, int64_t sb, kp<uint64_t> ptrs,
                                           kp<double> wt, char* ring, double (&acc)[kVE][kJB]) {
-#if PERS_SPLIT
+#if PERS_RING_SPLIT == 1
   fold_ring_split<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
+  return;
+#elif PERS_RING_SPLIT == 2
+  fold_ring_ahead<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
   return;
 #endif
   using G = Glds<T>;
@@ -593,7 +648,7 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 
   if constexpr (RING) {
     fold_ring<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
-  } else if constexpr (PERS_SPLIT != 0) {
+  } else {
     // the register pipeline (client slices loaded one group ahead) with the split weight loads
     // of fold_ring_split: each lgkmcnt(0) wait comes after half a client's folds
     constexpr int H = kJB / 2;
@@ -638,33 +693,6 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-  } else {
-  RT nxt[kU];
-#pragma unroll
-  for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[u], sb, zeros), e, count);
-  for (int k = 0; k < a.Npad; k += kU) {
-    RT cur[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) cur[u] = nxt[u];
-    const int kn = (k + kU < a.Npad) ? k + kU : k;  // the last group re-loads itself (L2 hits)
-#pragma unroll
-    for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[kn + u], sb, zeros), e, count);
-    // keep the next group's loads ahead of this group's folds (the scheduler would otherwise
-    // sink them to the next iteration, next to their use)
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      double x[kVE];
-      R::expand(cur[u], x);
-      const kp<double> wk = wt + static_cast<int64_t>(k + u) * a.wstride;
-#pragma unroll
-      for (int j = 0; j < kJB; ++j) {
-        const double wj = wk[j];
-#pragma unroll
-        for (int v = 0; v < kVE; ++v) acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wj);
-      }
-    }
-  }
   }
 
   bool in[kVE];

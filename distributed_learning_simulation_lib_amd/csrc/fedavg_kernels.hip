@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -1769,7 +1770,8 @@ struct Staged {
   bool clients_aligned = true;  // every client pointer is 16-byte aligned
   bool delta = false;           // clients are deltas against tab.base (fp64)
   int32_t max_weight_bits = 0;  // largest significand (bits) among the call's weights
-  bool weights_tame = true;     // every weight finite, zero or within [2^-800, 2^800]   // every client/out pointer is 16-byte aligned
+  bool weights_tame = true;     // every weight finite, zero or within [2^-800, 2^800]
+  double last_weight = std::numeric_limits<double>::quiet_NaN();  // note_weight's repeat cache
   std::vector<int32_t> kseg;
 };
 
@@ -1792,16 +1794,25 @@ namespace {
 
 // Significand width of a weight (bits between its leading and trailing one).
 void note_weight(Staged& st, double w) {
+  // called for every (client, tensor) entry of a call (thousands per wave): a client's weight
+  // usually repeats across its tensors, and the significand width comes from the bits directly
+  // (frexp / ldexp library calls cost ~20 ns per entry)
+  if (w == st.last_weight) return;
+  st.last_weight = w;
   if (w == 0.0) return;
-  if (!std::isfinite(w)) {
+  uint64_t b;
+  std::memcpy(&b, &w, sizeof(b));
+  const int be = static_cast<int>((b >> 52) & 0x7ff);
+  if (be == 0x7ff) {  // inf / NaN
     st.weights_tame = false;
     return;
   }
-  int e = 0;
-  const double m = std::frexp(std::fabs(w), &e);  // m in [0.5, 1)
-  if (e < -800 || e > 800) st.weights_tame = false;
-  uint64_t bits = static_cast<uint64_t>(std::ldexp(m, 53));  // exact: 53-bit integer
-  const int q = 53 - __builtin_ctzll(bits);
+  // |w| = m * 2^e with m in [0.5, 1) (frexp's convention): e = be - 1022 for normal w; a
+  // subnormal is far below 2^-800 anyway
+  const int e = be - 1022;
+  if (be == 0 || e < -800 || e > 800) st.weights_tame = false;
+  const uint64_t sig = (b & ((uint64_t(1) << 52) - 1)) | (be ? (uint64_t(1) << 52) : 0);
+  const int q = sig ? 53 - __builtin_ctzll(sig) : 0;
   st.max_weight_bits = std::max(st.max_weight_bits, q);
 }
 

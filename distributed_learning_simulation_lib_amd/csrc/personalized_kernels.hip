@@ -403,14 +403,7 @@ struct Glds<float> {
   __device__ __forceinline__ static void issue(uint64_t base, int lane, char* slot) {
     __builtin_amdgcn_global_load_lds((void PERS_AS_GLOBAL*)(base + lane * 16), (void __attribute__((address_space(3)))*)slot, 16, 0, 0);
   }
-  __device__ __forceinline__ static void read(const char* slot, int lane, double* x) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(slot + lane * 16);
-    x[0] = v.x;
-    x[1] = v.y;
-    x[2] = v.z;
-    x[3] = v.w;
-  }
-  // the split fold reads a slice one client ahead and widens it only after its wait
+  // a slice is read one client ahead and widened only after its wait
   using RawT = f32x4;
   __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
     return *reinterpret_cast<const f32x4*>(slot + lane * 16);
@@ -433,14 +426,6 @@ struct Glds<double> {
     __builtin_amdgcn_global_load_lds((void PERS_AS_GLOBAL*)(base + lane * 32 + 16),
                                      (void __attribute__((address_space(3)))*)(slot + 1024), 16, 0, 0);
   }
-  __device__ __forceinline__ static void read(const char* slot, int lane, double* x) {
-    const f64x2 lo = *reinterpret_cast<const f64x2*>(slot + lane * 16);
-    const f64x2 hi = *reinterpret_cast<const f64x2*>(slot + 1024 + lane * 16);
-    x[0] = lo.x;
-    x[1] = lo.y;
-    x[2] = hi.x;
-    x[3] = hi.y;
-  }
   using RawT = f64x2x2;
   __device__ __forceinline__ static RawT read_raw(const char* slot, int lane) {
     return RawT{*reinterpret_cast<const f64x2*>(slot + lane * 16), *reinterpret_cast<const f64x2*>(slot + 1024 + lane * 16)};
@@ -455,12 +440,9 @@ struct Glds<double> {
 template <typename T>
 constexpr bool kHasGlds = std::is_same<T, float>::value || std::is_same<T, double>::value;
 
-// The main loop on the LDS ring: acc[v][j] += x_k[v] * w_kj for every client k of the
-// (padded) list, in order. Requires a whole chunk and 16-B aligned client pointers.
-#ifndef PERS_RING_SPLIT  // ring loop A/B: 0 = one wait per client, 1 = halves, 2 = next client's weights ahead
-#define PERS_RING_SPLIT 1
-#endif
-// The ring fold with the weight loads hidden under the FMAs. Scalar loads complete out of order,
+// The main loop on the LDS ring: acc[v][j] += x_k[v] * w_kj for every client k of the (padded)
+// list, in order (whole chunks, 16-B aligned client pointers), with the weight loads hidden under
+// the FMAs. Scalar loads complete out of order,
 // so a wave can only wait for all of them at once (lgkmcnt(0)): loading a client's 16 weights and
 // then waiting exposes the scalar-load latency once per client. Here the receivers are split in
 // halves: while the low half's 32 FMAs of client c run, the high half's weights of c load; while
@@ -526,106 +508,6 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
   }
 }
 
-// PERS_RING_SPLIT == 2: client k + 1's weights (both halves) and x slice load while client k's
-// 64 folds run (64 weight SGPRs live instead of 32).
-template <typename T, int FOLD>
-__device__ __forceinline__ void fold_ring_ahead(const PArgs& a, int wave, int lane, int64_t sb, kp<uint64_t> ptrs,
-                                                kp<double> wt, char* ring, double (&acc)[kVE][kJB]) {
-  using G = Glds<T>;
-  const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
-  const int waves = a.waves;
-  const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
-  const int nst = a.Npad / kSC;
-  auto issue = [&](int st) {
-    char* stage = ring + (st % kRS) * (kSC * G::kSlice);
-    for (int i = 0; i < per; ++i) {
-      const int c = wave + i * waves;
-      const uint64_t p = ptrs[st * kSC + c];
-      G::issue(p ? p + sb : zeros, lane, stage + c * G::kSlice);
-    }
-  };
-  auto enter = [&](int st) {
-    if (st + kD < nst) issue(st + kD);
-    const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;
-    wait_vmcnt(ahead * per * G::kIPC);
-    __builtin_amdgcn_s_barrier();
-  };
-  auto slot = [&](int k) { return ring + ((k / kSC) % kRS) * (kSC * G::kSlice) + (k % kSC) * G::kSlice; };
-  for (int st = 0; st < kD && st < nst; ++st) issue(st);
-  enter(0);
-  typename G::RawT xr = G::read_raw(slot(0), lane);
-  double w[kJB];
-#pragma unroll
-  for (int j = 0; j < kJB; ++j) w[j] = wt[j];
-  const int n = a.Npad;
-#pragma unroll 1
-  for (int k = 0; k < n; ++k) {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): x slice and weights of k
-    __builtin_amdgcn_sched_barrier(0);
-    double x[kVE], wc[kJB];
-    G::expand(xr, x);
-#pragma unroll
-    for (int j = 0; j < kJB; ++j) wc[j] = w[j];
-    const int kn = k + 1 < n ? k + 1 : k;
-    if (kn != k && kn % kSC == 0) enter(kn / kSC);
-    xr = G::read_raw(slot(kn), lane);
-    const kp<double> wn = wt + static_cast<int64_t>(kn) * a.wstride;
-#pragma unroll
-    for (int j = 0; j < kJB; ++j) w[j] = wn[j];
-    __builtin_amdgcn_sched_barrier(0);
-    fold_half<FOLD, 0, kJB, false>(acc, x, wc);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-template <typename T, int FOLD>
-__device__ __forceinline__ void fold_ring(const PArgs& a, int wave, int lane, int64_t sb, kp<uint64_t> ptrs,
-                                          kp<double> wt, char* ring, double (&acc)[kVE][kJB]) {
-#if PERS_RING_SPLIT == 1
-  fold_ring_split<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
-  return;
-#elif PERS_RING_SPLIT == 2
-  fold_ring_ahead<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
-  return;
-#endif
-  using G = Glds<T>;
-  const uint64_t zeros = reinterpret_cast<uint64_t>(a.zeros);
-  const int waves = a.waves;
-  // this wave's clients of a stage: c = wave, wave + waves, ... < kSC (a wave-uniform count that
-  // may differ between waves, e.g. 2 / 1 / 1 at 3 waves; waves >= kSC: waves < kSC issue one,
-  // the others none) — each wave waits for its own DMAs only, the barrier for the rest
-  const int per = wave < kSC ? (kSC - wave + waves - 1) / waves : 0;
-  const int nst = a.Npad / kSC;
-  auto issue = [&](int st) {
-    char* stage = ring + (st % kRS) * (kSC * G::kSlice);
-    for (int i = 0; i < per; ++i) {
-      const int c = wave + i * waves;
-      const uint64_t p = ptrs[st * kSC + c];
-      G::issue(p ? p + sb : zeros, lane, stage + c * G::kSlice);
-    }
-  };
-  for (int st = 0; st < kD && st < nst; ++st) issue(st);
-  for (int st = 0; st < nst; ++st) {
-    if (st + kD < nst) issue(st + kD);
-    const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;  // stages issued after st
-    wait_vmcnt(ahead * per * G::kIPC);  // this wave's slices of stage st have landed
-    __builtin_amdgcn_s_barrier();        // ... and every other wave's
-    const char* stage = ring + (st % kRS) * (kSC * G::kSlice);
-#pragma unroll 1
-    for (int c = 0; c < kSC; ++c) {
-      double x[kVE];
-      G::read(stage + c * G::kSlice, lane, x);
-      const kp<double> wk = wt + static_cast<int64_t>(st * kSC + c) * a.wstride;
-#pragma unroll
-      for (int j = 0; j < kJB; ++j) {
-        const double wj = wk[j];
-#pragma unroll
-        for (int v = 0; v < kVE; ++v) acc[v][j] = pfold<FOLD>(acc[v][j], x[v], wj);
-      }
-    }
-  }
-}
-
 template <typename T, int FOLD, bool FULL, bool RING>
 __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, int seg, int count, int64_t start,
                                           double* chain, char* ring) {
@@ -647,7 +529,7 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
     for (int j = 0; j < kJB; ++j) acc[v][j] = -0.0;
 
   if constexpr (RING) {
-    fold_ring<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
+    fold_ring_split<T, FOLD>(a, wave, lane, sb, ptrs, wt, ring, acc);
   } else {
     // the register pipeline (client slices loaded one group ahead) with the split weight loads
     // of fold_ring_split: each lgkmcnt(0) wait comes after half a client's folds

@@ -422,8 +422,12 @@ class FedAvgContext:
             need = [int(nbytes(n)) for n in self.layout.numels]
             table.validate(need, 1, dev, ("record", tuple(need), dev))
         else:
-            esize = torch.empty((), dtype=in_dtype).element_size()
-            table.validate(self.layout.numels, esize, dev, (in_dtype, tuple(self.layout.numels), dev))
+            # the key is built once per (dtype, device): this runs per wave launch
+            keys = self.__dict__.setdefault("_dense_keys", {})
+            key = keys.get((in_dtype, dev))
+            if key is None:
+                key = keys[(in_dtype, dev)] = (in_dtype, tuple(self.layout.numels), dev)
+            table.validate(self.layout.numels, in_dtype.itemsize, dev, key)
 
     # -- hot path --------------------------------------------------------------------
     def accumulate(self, table: ClientTable, in_dtype: torch.dtype) -> None:

@@ -60,6 +60,24 @@ def reset(self, *a, **k):
 
 
 FedAvgContext.aggregate, FedAvgContext.raise_on_nan, FedAvgContext.reset = agg, nan, reset
+# the pieces after the flags are read: the rest of _finish_native, of _aggregate_parameter, and of
+# aggregate_worker_data (other_data + the result message)
+_fin, _aggp = FedAVGAlgorithm._finish_native, FedAVGAlgorithm._aggregate_parameter
+
+
+def fin(self, *a, **k):
+    r = _fin(self, *a, **k)
+    marks["fin_out"] = time.perf_counter()
+    return r
+
+
+def aggp(self, *a, **k):
+    r = _aggp(self, *a, **k)
+    marks["aggp_out"] = time.perf_counter()
+    return r
+
+
+FedAVGAlgorithm._finish_native, FedAVGAlgorithm._aggregate_parameter = fin, aggp
 algo = FedAVGAlgorithm(device=dev, wave_size=WAVE, wave_min=WAVE_MIN)
 msgs = lambda: [ParameterMessage(parameter=dict(p), aggregation_weight=x) for p, x in zip(params, w)]  # noqa: E731
 for _ in range(3):
@@ -71,7 +89,8 @@ torch.cuda.synchronize()
 ctx = algo._context()
 ctx.prof_collect()
 ctx.prof_enable(True)
-acc = {k: 0.0 for k in ("process", "to_agg", "aggregate_call", "between", "sync_and_flags", "after", "clear", "round")}
+acc = {k: 0.0 for k in ("process", "to_agg", "aggregate_call", "between", "sync_and_flags", "after", "after_finish",
+                        "after_aggregate_parameter", "after_message", "clear", "round")}
 for _ in range(R):
     ms = msgs()
     t0 = time.perf_counter()
@@ -88,6 +107,9 @@ for _ in range(R):
     acc["between"] += marks["nan_in"] - marks["agg_out"]
     acc["sync_and_flags"] += marks["nan_out"] - marks["nan_in"]
     acc["after"] += t2 - marks["nan_out"]
+    acc["after_finish"] += marks["fin_out"] - marks["nan_out"]
+    acc["after_aggregate_parameter"] += marks["aggp_out"] - marks["fin_out"]
+    acc["after_message"] += t2 - marks["aggp_out"]
     acc["clear"] += t3 - t2
     acc["round"] += t3 - t0
 torch.cuda.synchronize()

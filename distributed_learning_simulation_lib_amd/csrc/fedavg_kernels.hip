@@ -170,6 +170,13 @@ struct KArgs {
   double* const* win_dst;
   const int32_t* win_edge;
   int32_t win_n;
+  // Peer exchange, own window (COMB kernels): after this entry's zero-initialised chain, the
+  // element's partials of the comb_n entries holding clients are summed in entry order from -0.0 —
+  // comb_src[h] (device h's partial in this device's receive slot, accumulator coordinates), this
+  // entry's own chain from registers at h == comb_self — then divided and stored like a final fold.
+  const double* const* comb_src;
+  int32_t comb_n;
+  int32_t comb_self;
 };
 
 enum OutKind : int { OUT_ACC = 0, OUT_F32 = 1, OUT_F64 = 2 };
@@ -422,7 +429,8 @@ __device__ __forceinline__ double fold(double acc, double x, double w, double ba
 // PARTV: a tile shorter than TILE whose count is a whole number of lane-vectors (LANES * N
 // elements): the grouped / pipelined fast path with the missing vectors guarded wave-uniformly
 // (the balanced tile tables end every launch with such tiles, see build_balanced_tiles).
-template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD, int TILEN = kTile1, bool PARTV = false>
+template <typename T, int OUT, int SPLIT, bool VEC, bool FULL, int FOLD, int TILEN = kTile1, bool PARTV = false,
+          bool COMB = false>
 __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, double* lds) {
   constexpr int AE = Geo<T, SPLIT, TILEN>::AE;
   constexpr int LANES = Geo<T, SPLIT, TILEN>::LANES;  // lanes sharing one client stream
@@ -646,6 +654,40 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
   }
   if (!have) return;  // nothing for this segment in this call (host prevents for finals)
 
+  if constexpr (COMB) {
+    // S_0 + S_1 + ... in entry order (multi_device.cpp's composition), this entry's chain in place
+    static_assert(OUT != OUT_ACC && SPLIT == 1, "the own-window combine ends a final fold");
+    double tot[AE];
+#pragma unroll
+    for (int i = 0; i < AE; ++i) tot[i] = -0.0;
+    for (int h = 0; h < a.comb_n; ++h) {  // wave-uniform
+      if (h == a.comb_self) {
+#pragma unroll
+        for (int i = 0; i < AE; ++i) tot[i] = tot[i] + acc[i];
+      } else {
+        const gptr<const double> sp =
+            to_global<double>(reinterpret_cast<const void*>(to_const<uint64_t>(a.comb_src)[h])) + acc_base;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          const int e = (v * LANES + li) * N;
+#pragma unroll
+          for (int j = 0; j < N; j += 2) {
+            if (FULL || e + j + 2 <= count) {
+              const f64x2 d = *(gptr<const f64x2>)(sp + e + j);
+              tot[v * N + j] = tot[v * N + j] + d.x;
+              tot[v * N + j + 1] = tot[v * N + j + 1] + d.y;
+            } else {
+              if (e + j < count) tot[v * N + j] = tot[v * N + j] + sp[e + j];
+              if (e + j + 1 < count) tot[v * N + j + 1] = tot[v * N + j + 1] + sp[e + j + 1];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < AE; ++i) acc[i] = tot[i];
+  }
+
   // fused NaN check on the accumulator (fed_avg_algorithm.py:93)
   bool bad_acc = false;
 #pragma unroll
@@ -753,7 +795,7 @@ __device__ __forceinline__ void tile_body(const KArgs& a, const TileDesc& td, do
 // a balanced order, build_balanced_tiles) and they take the grouped fast path. A separate
 // instantiation: compiled into every launch, that path cost the plain whole-layout launch 3-4 %
 // (VGPRs 131 -> 144, twice the code; profiles/r03_ab_matrix.txt).
-template <typename T, int OUT, int SPLIT, bool VEC, int FOLD, int TILEN = kTile1, bool PV = false>
+template <typename T, int OUT, int SPLIT, bool VEC, int FOLD, int TILEN = kTile1, bool PV = false, bool COMB = false>
 __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS)) void fedavg_tile_kernel(KArgs a) {
   __shared__ double lds[(SPLIT > 1) ? ((SPLIT - 1) * 64 * kAE + 8) : 1];
   constexpr int TILE = Geo<T, SPLIT, TILEN>::TILE;
@@ -777,6 +819,13 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS)) void fedavg_tile_k
       }
       return;
     }
+  }
+  if constexpr (COMB) {
+    // own-window combine launches: one tile per workgroup, exact order, no balanced pieces
+    const TileDesc td = load_tile(a.tiles, a.tile_begin + static_cast<int>(blockIdx.x));
+    if (td.count == TILE) tile_body<T, OUT, SPLIT, VEC, true, FOLD, TILEN, false, true>(a, td, lds);
+    else tile_body<T, OUT, SPLIT, VEC, false, FOLD, TILEN, false, true>(a, td, lds);
+    return;
   }
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const TileDesc td = load_tile(a.tiles, a.tile_begin + (t < a.walk_back ? a.walk_back - 1 - t : t));
@@ -1782,6 +1831,7 @@ struct fedavg_plan {
   fedavg_ctx* ctx = nullptr;
   int device = -1;  // the context's device (destroy must not read a context freed before it)
   Staged st;
+  std::vector<char> fin_img;  // totals + outputs last copied into the blob (own-window combine)
   char* dev = nullptr;
   int32_t in_dtype = 0;
   int out_kind = 0;
@@ -2037,6 +2087,38 @@ hipError_t launch_out(int32_t in_dtype, const KArgs& a, int split, bool vec, int
   }
 }
 
+// Own-window combine launches of the multi-device peer exchange (KArgs::comb_*): exact order,
+// one tile per workgroup, scalar-weight folds only (no delta calls).
+template <typename T, int OUT>
+hipError_t launch_comb_typed(const KArgs& a, bool vec, int fold, hipStream_t s, hipEvent_t e1) {
+  if constexpr (OUT == OUT_ACC) {
+    return hipErrorInvalidValue;
+  } else {
+    const dim3 grid(static_cast<unsigned>(a.num_tiles)), block(Geo<T, 1, kTile1>::THREADS);
+    if (fold == FOLD_FMA) {
+      if (vec) hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, true, FOLD_FMA, kTile1, false, true>), grid, block, 0, s, nullptr, e1, 0, a);
+      else hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, false, FOLD_FMA, kTile1, false, true>), grid, block, 0, s, nullptr, e1, 0, a);
+    } else if (fold == FOLD_MULADD) {
+      if (vec) hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, true, FOLD_MULADD, kTile1, false, true>), grid, block, 0, s, nullptr, e1, 0, a);
+      else hipExtLaunchKernelGGL((fedavg_tile_kernel<T, OUT, 1, false, FOLD_MULADD, kTile1, false, true>), grid, block, 0, s, nullptr, e1, 0, a);
+    } else {
+      return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+}
+
+template <int OUT>
+hipError_t launch_comb_out(int32_t in_dtype, const KArgs& a, bool vec, int fold, hipStream_t s, hipEvent_t e1) {
+  switch (in_dtype) {
+    case FEDAVG_F32: return launch_comb_typed<float, OUT>(a, vec, fold, s, e1);
+    case FEDAVG_F16: return launch_comb_typed<__half, OUT>(a, vec, fold, s, e1);
+    case FEDAVG_BF16: return launch_comb_typed<bf16_t, OUT>(a, vec, fold, s, e1);
+    case FEDAVG_F64: return launch_comb_typed<double, OUT>(a, vec, fold, s, e1);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 bool is_qsgd(int32_t dt) { return dt == FEDAVG_QSGD_F32 || dt == FEDAVG_QSGD_F64; }
 bool is_nnadq(int32_t dt) { return dt == FEDAVG_NNADQ_F32 || dt == FEDAVG_NNADQ_F64; }
 bool is_record(int32_t dt) { return is_qsgd(dt) || is_nnadq(dt); }
@@ -2093,9 +2175,14 @@ int choose_split(const fedavg_ctx* c, int kmax) {
 int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_dtype, int out_kind,
                     int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1,
                     hipEvent_t* done_ev = nullptr, double* acc_out = nullptr,
-                    const KArgs* win = nullptr) {
+                    const KArgs* win = nullptr, const KArgs* comb = nullptr) {
   if (st.delta) split = 1;  // delta folds run the exact-order kernel only
+  if (comb) split = 1;
   KArgs a;
+  // comb (dense final folds only): the multi-device own-window combine (KArgs::comb_*)
+  a.comb_src = comb ? comb->comb_src : nullptr;
+  a.comb_n = comb ? comb->comb_n : 0;
+  a.comb_self = comb ? comb->comb_self : 0;
   a.segs = c->d_segs;
   a.tab = st.tab;
   // win (dense zero-initialised partials only): the multi-device window table (KArgs::win_dst)
@@ -2124,7 +2211,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   }
   // whole-layout exact-order launch of a 2- / 4-byte input: the wide table (same elements)
   // (a windowed launch indexes the exact-order table: no wide / balanced / reversed orders)
-  const bool wide = !win && split == 1 && c->d_tilesw != nullptr && tb_split1 == 0 &&
+  const bool wide = !win && !comb && split == 1 && c->d_tilesw != nullptr && tb_split1 == 0 &&
                     st.Kmax >= c->wide_min_clients &&
                     te_split1 == static_cast<int32_t>(c->tiles1.size()) &&
                     (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F16 || in_dtype == FEDAVG_BF16 ||
@@ -2137,7 +2224,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
       a.tiles = c->d_tilesw_bal;
       te = static_cast<int>(c->tilesw_bal.size());
     }
-  } else if (!win && split == 1 && in_dtype == FEDAVG_F64 && c->d_tiles1_bal != nullptr &&
+  } else if (!win && !comb && split == 1 && in_dtype == FEDAVG_F64 && c->d_tiles1_bal != nullptr &&
              tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
     a.tiles = c->d_tiles1_bal;  // a whole-layout fp64 launch: the balanced order of the same tiles
     tb = 0;
@@ -2149,7 +2236,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   // whole-layout waves alternate their walk (a balanced order reverses only its leading whole
   // waves: its short pieces stay at the end, where they balance the tail; ranged launches keep
   // their order)
-  if (!win && c->walk_alternate && split == 1 && !is_record(in_dtype) &&
+  if (!win && !comb && c->walk_alternate && split == 1 && !is_record(in_dtype) &&
       tb_split1 == 0 && te_split1 == static_cast<int32_t>(c->tiles1.size())) {
     if (c->walk_reverse)
       a.walk_back = (a.tiles == c->d_tilesw_bal)   ? c->tilesw_bal_head
@@ -2172,7 +2259,7 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
     e1 = nullptr;
   }
   hipError_t err = hipSuccess;
-  if (is_record(in_dtype) && win) return fail(FEDAVG_ERR_INVALID, "windowed launches take dense inputs");
+  if (is_record(in_dtype) && (win || comb)) return fail(FEDAVG_ERR_INVALID, "windowed launches take dense inputs");
   if (is_record(in_dtype)) {
     // quantised records: one tile per workgroup, exact client order (no split); the record layout needs 16-B aligned records; outputs may be unaligned
     if (st.delta) return fail(FEDAVG_ERR_INVALID, "quantised records cannot be delta updates");
@@ -2246,6 +2333,20 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
   const int fold = st.delta ? FOLD_DELTA
                             : (c->allow_fma && fma_exact_call(st, in_dtype)) ? FOLD_FMA : FOLD_MULADD;
   const bool partv = a.tiles == c->d_tilesw_bal || a.tiles == c->d_tiles1_bal;  // a balanced order
+  if (comb) {
+    if (st.delta) return fail(FEDAVG_ERR_INVALID, "the own-window combine takes scalar-weight folds");
+    switch (out_kind) {
+      case OUT_F32: err = launch_comb_out<OUT_F32>(in_dtype, a, st.aligned, fold, s, e1); break;
+      case OUT_F64: err = launch_comb_out<OUT_F64>(in_dtype, a, st.aligned, fold, s, e1); break;
+      default: return fail(FEDAVG_ERR_INVALID, "the own-window combine writes fp32 / fp64 outputs");
+    }
+    if (err != hipSuccess) return fail(FEDAVG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(err));
+    if (m1) {
+      FEDAVG_HIP_TRY(hipEventRecord(m1, s));
+      if (done_ev) *done_ev = m1;
+    }
+    return FEDAVG_OK;
+  }
   switch (out_kind) {
     case OUT_ACC: err = launch_out<OUT_ACC>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide, partv); break;
     case OUT_F32: err = launch_out<OUT_F32>(in_dtype, a, split, st.aligned, fold, nblocks, s, nullptr, e1, wide, partv); break;
@@ -3227,6 +3328,56 @@ __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_windows(f
   return launch_main(c, static_cast<hipStream_t>(stream), p->st, p->in_dtype, p->out_kind, 1, 1, tb, te, nullptr,
                      nullptr, &win);
 }
+// Shared with multi_device.cpp: the own window of the peer exchange. Plan p's clients are folded
+// over tiles [tb, te) from -0.0 and, per element, summed in entry order with the other entries'
+// partials (comb_src: a device array of comb_n slot pointers, this entry at comb_self), divided
+// by totals[seg] and stored into outs[seg] (host tables of T entries; copied into the plan's own
+// table blob when they change) — fed_avg_algorithm.py:43-64 then :71-97 for this window.
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_comb(fedavg_plan* p, int32_t tb, int32_t te,
+                                                                          void* stream, const double* const* comb_src,
+                                                                          int32_t comb_n, int32_t comb_self,
+                                                                          const double* totals, void* const* outs,
+                                                                          int32_t out_dtype) {
+  if (!p || !p->ctx) return fail(FEDAVG_ERR_INVALID, "null plan");
+  if (p->kind != fedavg_plan::PARTIAL || !p->zero_init)
+    return fail(FEDAVG_ERR_INVALID, "the multi-device exchange takes zero-initialised partial plans");
+  if (is_record(p->in_dtype) || p->st.delta) return fail(FEDAVG_ERR_INVALID, "the own-window combine takes dense folds");
+  const int ok = out_kind_of(out_dtype);
+  if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+  if (comb_n < 1 || comb_self < 0 || comb_self >= comb_n || !comb_src || !totals || !outs)
+    return fail(FEDAVG_ERR_INVALID, "bad combine table");
+  fedavg_ctx* c = p->ctx;
+  const int32_t nt = static_cast<int32_t>(c->tiles1.size());
+  if (tb < 0 || tb > te || te > nt) return fail(FEDAVG_ERR_INVALID, "bad tile range");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int T = c->T;
+  // the plan blob's totals / outputs sections (a partial plan leaves them 1.0 / NULL)
+  const BlobLayout L(T, std::max(p->st.stride, 1));
+  std::vector<char> img(sizeof(double) * T + sizeof(void*) * T);
+  std::memcpy(img.data(), totals, sizeof(double) * T);
+  std::memcpy(img.data() + sizeof(double) * T, outs, sizeof(void*) * T);
+  bool outs16 = true;
+  for (int t = 0; t < T; ++t) {
+    if (!outs[t]) return fail(FEDAVG_ERR_INVALID, "null output pointer");
+    if (reinterpret_cast<uintptr_t>(outs[t]) % 16) outs16 = false;
+  }
+  if (p->fin_img != img) {
+    FEDAVG_HIP_TRY(hipStreamSynchronize(s));  // an earlier combine on this stream may read the old tables
+    FEDAVG_HIP_TRY(hipMemcpy(p->dev + L.off_wtot, img.data(), sizeof(double) * T, hipMemcpyHostToDevice));
+    FEDAVG_HIP_TRY(hipMemcpy(p->dev + L.off_outs, img.data() + sizeof(double) * T, sizeof(void*) * T,
+                             hipMemcpyHostToDevice));
+    p->fin_img = img;
+  }
+  Staged st = p->st;
+  st.aligned = st.aligned && outs16;
+  KArgs comb{};
+  comb.comb_src = comb_src;
+  comb.comb_n = comb_n;
+  comb.comb_self = comb_self;
+  return launch_main(c, s, st, p->in_dtype, ok, 1, 1, tb, te, nullptr, nullptr, nullptr, &comb);
+}
+
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_is_record(const fedavg_plan* p) {
   return (p && is_record(p->in_dtype)) ? 1 : 0;
 }

@@ -7,19 +7,21 @@
 // high-priority exchange stream per entry, and the peer mappings between the devices.
 //
 // The PEER exchange (no collective library): chunk k of the tile table is cut into G windows and
-// device j owns window j. Per chunk, device g runs one partial launch over the chunk whose tiles of
-// window j store their fp64 partial straight into device j's receive slot for g over xGMI (the
-// store address is a peer mapping picked per tile from a window table; device g's own window goes
-// into its own slot). An event after
-// device g's chunk k orders the exchange stream of every device j behind it; device j's exchange
-// stream then sums the G partials of its window in device order, divides and stores the result
-// into the root's outputs (a peer store for j != root). Per round, HBM carries on each device its
-// clients, (G-1)/G of the fp64 partial arriving from peers plus its own window, one read of its G
-// slot windows and 1/G of the result — no fp64 partial is written and re-read whole, and no copy
-// engine or collective kernel sits between the fold and the division.
+// device j owns window j. Per chunk, device g first folds the chunk's OTHER windows (a launch on
+// each side of its own): each tile's fp64 partial is stored straight into the window owner's receive
+// slot for g over xGMI (the store address is a peer mapping picked per tile from a window table).
+// An event after those launches orders every other device's exchange stream behind them. Device j's
+// exchange stream then folds its own window of chunk k — its clients from -0.0 — and, per element,
+// adds the received partials of the other devices in device order (its own chain taken from
+// registers at its place), divides, and stores the result into the root's outputs (a peer store for
+// j != root). Per round, HBM carries on each device its clients, the (G-1)/G of the fp64 partial
+// arriving from peers, one read of it, and 1/G of the result — no fp64 partial is written and
+// re-read whole, no own-window partial at all, and no copy engine or collective kernel sits between
+// the fold and the division. Quantised-record plans keep the older form: every
+// window (their own included) into the owner's slot, then a separate combine kernel.
 //
-//   exchange stream j : (wait part[0..G-1][k]) combine(window j of chunk k) ... -> done[j]
-//   stream g          : partial(chunk k: every window to its owner's slot) -> part[g][k]
+//   exchange stream j : (wait part[g != j][k]) fold own window of chunk k + combine ... -> done[j]
+//   stream g          : partial(chunk k, the other windows: each to its owner's slot) -> part[g][k]
 //
 // The REDUCE exchange keeps the per-process path's arithmetic: each chunk's partial is reduced to
 // the root's accumulator by an in-process RCCL communicator (ncclCommInitAll, grouped calls from
@@ -45,6 +47,11 @@ __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_windows(f
                                                                              void* stream, double* const* dst,
                                                                              const int32_t* edge, int32_t n);
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_is_record(const fedavg_plan* p);
+__attribute__((visibility("hidden"))) int32_t fedavg_internal_plan_run_comb(fedavg_plan* p, int32_t tb, int32_t te,
+                                                                          void* stream, const double* const* comb_src,
+                                                                          int32_t comb_n, int32_t comb_self,
+                                                                          const double* totals, void* const* outs,
+                                                                          int32_t out_dtype);
 __attribute__((visibility("hidden"))) int32_t fedavg_internal_multi_combine(fedavg_ctx* c, int32_t tb, int32_t te,
                                                                           const double* const* slots, int32_t G,
                                                                           const double* wtot, void* const* outs,
@@ -96,6 +103,10 @@ struct fedavg_multi {
   std::vector<char*> win_dev;
   std::vector<size_t> win_cap;
   std::vector<std::vector<char>> win_host;
+  // per entry j: the own-window combine's source table — slots[j][h] for the round's members h —
+  // on device j, and its host image
+  std::vector<char*> comb_dev;
+  std::vector<std::vector<char>> comb_host;
   bool any_round = false;
   // in-process RCCL (REDUCE exchange)
   std::vector<ncclComm_t> nccl;
@@ -173,6 +184,22 @@ int32_t upload_windows(fedavg_multi* m, const std::vector<int32_t>& edges) {
     }
     MULTI_HIP_TRY(hipMemcpy(m->win_dev[g], img.data(), img.size(), hipMemcpyHostToDevice));
     m->win_host[g] = img;
+  }
+  return FEDAVG_OK;
+}
+
+// Entry j's own-window combine sources for this round's members (re-uploaded when they change,
+// after entry j's exchange stream stopped reading the old table).
+int32_t upload_comb(fedavg_multi* m, const std::vector<int32_t>& members) {
+  for (int32_t j = 0; j < m->G; ++j) {
+    std::vector<char> img(sizeof(double*) * FEDAVG_MULTI_MAX_DEVICES, 0);
+    for (size_t i = 0; i < members.size(); ++i) std::memcpy(img.data() + sizeof(double*) * i, &m->slots[j][members[i]], sizeof(double*));
+    if (m->comb_host[j] == img) continue;
+    MULTI_HIP_TRY(hipSetDevice(m->devices[j]));
+    MULTI_HIP_TRY(hipStreamSynchronize(m->xstr[j]));
+    if (!m->comb_dev[j]) MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->comb_dev[j]), img.size()));
+    MULTI_HIP_TRY(hipMemcpy(m->comb_dev[j], img.data(), img.size(), hipMemcpyHostToDevice));
+    m->comb_host[j] = img;
   }
   return FEDAVG_OK;
 }
@@ -315,6 +342,8 @@ int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t 
   m->win_dev.assign(m->G, nullptr);
   m->win_cap.assign(m->G, 0);
   m->win_host.assign(m->G, {});
+  m->comb_dev.assign(m->G, nullptr);
+  m->comb_host.assign(m->G, {});
   auto bail = [&](int32_t st) {
     fedavg_multi_destroy(m);
     return st;
@@ -380,6 +409,7 @@ int32_t fedavg_multi_destroy(fedavg_multi* m) {
       if (m->slot_owned[j][g] && m->slots[j][g]) (void)hipFree(m->slots[j][g]);
     if (m->tab_dev[j]) (void)hipFree(m->tab_dev[j]);
     if (m->win_dev[j]) (void)hipFree(m->win_dev[j]);
+    if (m->comb_dev[j]) (void)hipFree(m->comb_dev[j]);
     for (hipEvent_t ev : m->part_ev[j]) (void)hipEventDestroy(ev);
     if (m->start_ev[j]) (void)hipEventDestroy(m->start_ev[j]);
     if (m->done_ev[j]) (void)hipEventDestroy(m->done_ev[j]);
@@ -436,8 +466,16 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
     if (int32_t st = ensure_part_events(m, chunks)) return st;
     if (int32_t st = upload_tables(m, total_weights, out_ptrs)) return st;
     if (int32_t st = upload_windows(m, edges)) return st;
+    if (int32_t st = upload_comb(m, members)) return st;
     if (int32_t st = order_round_start(m, streams)) return st;
     const int32_t vec = outs_aligned(out_ptrs, m->T, out_dtype) ? 1 : 0;
+    // a member with a dense plan folds its own window last, with the other members' partials of
+    // it added in entry order in the same kernel (no own-window slot store and re-read)
+    std::vector<int32_t> fused(m->G, 0), rank_of(m->G, -1);
+    for (size_t i = 0; i < members.size(); ++i) {
+      rank_of[members[i]] = static_cast<int32_t>(i);
+      fused[members[i]] = fedavg_internal_plan_is_record(partials[members[i]]) ? 0 : 1;
+    }
     for (int32_t k = 0; k < chunks; ++k) {
       const int64_t tb = edges[k], span = edges[k + 1] - edges[k];
       auto window = [&](int32_t j, int32_t& wb, int32_t& we) {
@@ -447,13 +485,20 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
       for (int32_t g : members) {
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
         hipStream_t s = stream_of(m, streams, g);
-        if (!fedavg_internal_plan_is_record(partials[g])) {
-          // one launch over the chunk: each tile stores into its window owner's slot
+        if (fused[g]) {
+          // the chunk's other windows: each tile stores into its window owner's slot (one launch
+          // on each side of the own window)
           const char* wt = m->win_dev[g];
-          if (int32_t st = fedavg_internal_plan_run_windows(
-                  partials[g], edges[k], edges[k + 1], s, reinterpret_cast<double* const*>(wt),
-                  reinterpret_cast<const int32_t*>(wt + sizeof(double*) * m->G) + k * (m->G + 1), m->G))
-            return st;
+          int32_t ob = 0, oe = 0;
+          window(g, ob, oe);
+          const int32_t ranges[2][2] = {{edges[k], ob}, {oe, edges[k + 1]}};
+          for (const auto& r : ranges) {
+            if (r[0] >= r[1]) continue;
+            if (int32_t st = fedavg_internal_plan_run_windows(
+                    partials[g], r[0], r[1], s, reinterpret_cast<double* const*>(wt),
+                    reinterpret_cast<const int32_t*>(wt + sizeof(double*) * m->G) + k * (m->G + 1), m->G))
+              return st;
+          }
         } else {
           for (int32_t r = 1; r <= m->G; ++r) {
             const int32_t j = (g + r) % m->G;  // quantised records: one launch per window, own last
@@ -471,6 +516,15 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
         window(j, wb, we);
         if (wb == we) continue;
         MULTI_HIP_TRY(hipSetDevice(m->devices[j]));
+        if (fused[j]) {
+          for (int32_t g : members)
+            if (g != j) MULTI_HIP_TRY(hipStreamWaitEvent(m->xstr[j], m->part_ev[g][k], 0));
+          if (int32_t st = fedavg_internal_plan_run_comb(
+                  partials[j], wb, we, m->xstr[j], reinterpret_cast<const double* const*>(m->comb_dev[j]),
+                  static_cast<int32_t>(members.size()), rank_of[j], total_weights, out_ptrs, out_dtype))
+            return st;
+          continue;
+        }
         for (int32_t g : members) MULTI_HIP_TRY(hipStreamWaitEvent(m->xstr[j], m->part_ev[g][k], 0));
         std::vector<const double*> src;
         for (int32_t g : members) src.push_back(m->slots[j][g]);

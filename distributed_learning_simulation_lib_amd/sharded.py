@@ -417,35 +417,43 @@ class ExchangeModel:
     def _peer_round_ms(self, G: int, numel: int, n_clients: int, in_bytes: int, out_bytes: int, fracs: list[float],
                        under: list[float], n_root: int, n_peer: int) -> dict[str, float]:
         """The single-process peer-window exchange (multi_device.cpp). Per chunk every
-        device folds its clients window by window, its partial of window j stored straight into
-        device j's receive slot (a peer store: the link carries S/G per peer per round, the
-        receiver's HBM takes it), then device j sums its G slot windows of the chunk and divides,
-        storing 1/G of the result into the root. A device's HBM per chunk: its clients + its own
-        window's partial + the (G-1) windows arriving from peers + the previous chunk's combine
-        (G slot windows read) + on the root all result windows; the fold of a chunk cannot end
-        before its peer stores have drained over the links. After the last chunk: its combine,
-        the result windows' trip to the root over one link each, and a cross-device hand-off."""
+        device folds its clients over the other windows, each tile's fp64 partial stored straight into
+        the window owner's receive slot (a peer store: S/G per peer link per round, the receiver's HBM
+        takes it), and then folds its own window with the G - 1 received partials of it added in entry
+        order in the same kernel, dividing and storing 1/G of the result into the root. A device's HBM
+        per chunk: its clients, the (G-1)/G of the chunk's partial arriving from peers, the own-window
+        kernel's read of those same bytes, and on the root every result window; the other windows'
+        fold cannot end before its peer stores have drained over the links. The last chunk's own-window
+        kernel (it waits for every peer's stores) and the result's trip to the root are the tail, plus
+        a cross-device hand-off."""
         link = self.link_rate * self.link_eff
         rate = self.fold_rate / 1e3
         part_b, res_b = numel * 8, numel * out_bytes
+        share = (G - 1) / G  # the partial bytes of a chunk a device receives (and its own window re-reads)
+
+        def own_window(f: float, n: int, root: bool) -> float:
+            """Bytes of one device's own-window kernel for a chunk of fraction f."""
+            return f / G * n * numel * in_bytes + share * f * part_b + (f * res_b if root else f * res_b / G)
+
         root_t = peer_t = 0.0
         for c, f in enumerate(fracs):
-            combine_prev = fracs[c - 1] * part_b if c else 0.0  # G slot windows of the last chunk
-            recv = f * part_b  # its own window + (G-1) windows from the peers
-            clients_root, clients_peer = f * n_root * numel * in_bytes, f * n_peer * numel * in_bytes
+            last = c == len(fracs) - 1
             drain = f * part_b / G / link * 1e3 if G > 1 else 0.0  # one window per peer link
-            root_t += max((clients_root + recv + combine_prev + (fracs[c - 1] * res_b if c else 0.0)) / rate,
-                          drain) + under[c]
-            peer_t += max((clients_peer + recv + combine_prev) / rate, drain) + under[c]
+            others_root = (1 - 1 / G) * f * n_root * numel * in_bytes + share * f * part_b
+            others_peer = (1 - 1 / G) * f * n_peer * numel * in_bytes + share * f * part_b
+            own_root = 0.0 if last else own_window(f, n_root, True)
+            own_peer = 0.0 if last else own_window(f, n_peer, False)
+            root_t += max((others_root + own_root) / rate, drain) + under[c]
+            peer_t += max((others_peer + own_peer) / rate, drain) + under[c]
         last = fracs[-1]
-        combine_last = (last * part_b + last * res_b / G) / rate
+        own_last = max(own_window(last, n_root, True), own_window(last, n_peer, False) if G > 1 else 0.0) / rate
         result_link = last * res_b / G / link * 1e3 if G > 1 else 0.0
         fold = max(root_t, peer_t if G > 1 else 0.0)
-        tail = combine_last + result_link + (self.sync_ms if G > 1 else 0.0)
+        tail = own_last + result_link + (self.sync_ms if G > 1 else 0.0)
         step = fold + tail
         t1 = self.one_gpu_ms(numel, n_clients, in_bytes, out_bytes)
         return {"fold_ms": round(fold, 4), "exposed_exchange_and_finalize_ms": round(tail, 4),
-                "last_chunk_exchange_ms": round(result_link, 4), "last_finalize_ms": round(combine_last, 4),
+                "last_chunk_exchange_ms": round(result_link, 4), "last_finalize_ms": round(own_last, 4),
                 "root_clients": n_root, "peer_clients": n_peer,
                 "step_ms": round(step, 4), "one_gpu_ms": round(t1, 4), "speedup": round(t1 / step, 3)}
 

@@ -463,12 +463,12 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
  *       one round of device-resident clients: partials[g] is a zero-initialised partial plan on
  *       context g (NULL = device g holds no client). Exchanges:
  *        FEDAVG_EXCHANGE_PEER  — chunk k (tiles [edges[k], edges[k+1])) is cut into G windows,
- *          device j owns window j. Device g's partial kernel for window j stores its fp64 partial
- *          straight into device j's receive slot over xGMI (own window last); device j then sums
- *          the G partials of its window in device order S_0 + S_1 + ... (deterministic),
- *          divides by totals[t] and stores the result into the root's outputs (a peer store).
- *          Cross-device order is carried by events (no spinning kernel). Needs peer access
- *          (or aliased devices).
+ *          device j owns window j. Device g's partial kernel for window j != g stores its fp64
+ *          partial straight into device j's receive slot over xGMI; device j then folds its own
+ *          window and, in the same kernel, sums the G partials of it in device order
+ *          S_0 + S_1 + ... (its own from registers; deterministic), divides by totals[t] and
+ *          stores the result into the root's outputs (a peer store). Cross-device order is
+ *          carried by events (no spinning kernel). Needs peer access (or aliased devices).
  *        FEDAVG_EXCHANGE_REDUCE — each chunk's partials are reduced to the root's accumulator by
  *          an in-process RCCL communicator (ncclCommInitAll, created on first use; RCCL's
  *          summation order), then the root divides.

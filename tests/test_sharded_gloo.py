@@ -455,7 +455,7 @@ def test_exchange_model_prices_the_peer_window_exchange():
         assert ex == "peer" and peer["speedup"] > rccl["speedup"] and peer["speedup"] < G
         assert peer["step_ms"] >= peer["fold_ms"] > 0
     (_, _, _), p4 = m.best(4, P, 256, 4, 4, tiles, exchange_candidates(exchanges=("peer",)))
-    assert p4["speedup"] >= 3.5
+    assert p4["speedup"] >= 3.6  # the own window folded with the received partials (no own-slot pass)
     # no link at all on one device: the fold alone plus the combine
     one = m.round_ms(1, P, 256, 4, 4, [0, tiles], "peer")
     assert one["last_chunk_exchange_ms"] == 0.0

@@ -472,17 +472,22 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
     wait_vmcnt(ahead * per * G::kIPC);
     __builtin_amdgcn_s_barrier();
   };
-  auto slot = [&](int k) { return ring + ((k / kSC) % kRS) * (kSC * G::kSlice) + (k % kSC) * G::kSlice; };
   for (int st = 0; st < kD && st < nst; ++st) issue(st);
   enter(0);
-  typename G::RawT xr = G::read_raw(slot(0), lane);
+  // the client slot, the ring stage and the weight row advance incrementally (no per-client
+  // division or 64-bit multiply in the scalar stream)
+  constexpr int kStage = kSC * G::kSlice;
+  const char* cur = ring;
+  int c_in = 0, ring_st = 0, st = 0;
+  kp<double> wk = wt;
+  const int64_t wstep = a.wstride;
+  typename G::RawT xr = G::read_raw(cur, lane);
   double wlo[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) wlo[j] = wt[j];
   const int n = a.Npad;
 #pragma unroll 1
   for (int k = 0; k < n; ++k) {
-    const kp<double> wk = wt + static_cast<int64_t>(k) * a.wstride;
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the x slice and the low weights of k
     __builtin_amdgcn_sched_barrier(0);
     double whi[H];
@@ -495,16 +500,30 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the high weights of k
     __builtin_amdgcn_sched_barrier(0);
-    // next client (the last one re-reads itself): its stage may need entering first
-    const int kn = k + 1 < n ? k + 1 : k;
-    if (kn != k && kn % kSC == 0) enter(kn / kSC);
-    xr = G::read_raw(slot(kn), lane);
-    const kp<double> wn = wt + static_cast<int64_t>(kn) * a.wstride;
+    // next client: the next slot of this stage, or the next stage's first (entered here); after
+    // the last client, this one again
+    const char* nxt = cur;
+    kp<double> wn = wk;
+    if (k + 1 < n) {
+      wn = wk + wstep;
+      if (c_in + 1 < kSC) {
+        nxt = cur + G::kSlice;
+        ++c_in;
+      } else {
+        enter(++st);
+        ring_st = ring_st + 1 == kRS ? 0 : ring_st + 1;
+        nxt = ring + ring_st * kStage;
+        c_in = 0;
+      }
+    }
+    xr = G::read_raw(nxt, lane);
 #pragma unroll
     for (int j = 0; j < H; ++j) wlo[j] = wn[j];
     __builtin_amdgcn_sched_barrier(0);
     fold_half<FOLD, H, H, false>(acc, x, whi);
     __builtin_amdgcn_sched_barrier(0);
+    cur = nxt;
+    wk = wn;
   }
 }
 

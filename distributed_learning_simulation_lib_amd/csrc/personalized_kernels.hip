@@ -560,6 +560,8 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 #pragma unroll
     for (int j = 0; j < H; ++j) wlo[j] = wt[j];
     const int n = a.Npad;
+    kp<double> wk = wt;  // weight row of client k + u, advanced incrementally
+    const int64_t wstep = a.wstride;
     for (int k = 0; k < n; k += kU) {
       RT cur[kU];
 #pragma unroll
@@ -573,7 +575,6 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
         const int kk = k + u;
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the low weights of kk
         __builtin_amdgcn_sched_barrier(0);
-        const kp<double> wk = wt + static_cast<int64_t>(kk) * a.wstride;
         double whi[H];
 #pragma unroll
         for (int j = 0; j < H; ++j) whi[j] = wk[H + j];
@@ -585,13 +586,13 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the high weights of kk
         __builtin_amdgcn_sched_barrier(0);
-        const int k1 = kk + 1 < n ? kk + 1 : kk;
-        const kp<double> w1 = wt + static_cast<int64_t>(k1) * a.wstride;
+        const kp<double> w1 = kk + 1 < n ? wk + wstep : wk;
 #pragma unroll
         for (int j = 0; j < H; ++j) wlo[j] = w1[j];
         __builtin_amdgcn_sched_barrier(0);
         fold_half<FOLD, H, H, false, !std::is_same<T, double>::value>(acc, x, whi);
         __builtin_amdgcn_sched_barrier(0);
+        wk = w1;
       }
     }
   }

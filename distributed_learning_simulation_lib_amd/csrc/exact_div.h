@@ -50,6 +50,35 @@ __device__ __forceinline__ double exact_div_fast(double a, const ExactDiv& d, bo
   return __builtin_fma(-t, d.y, q0);
 }
 
+// exact_div_prepare with the reciprocal RN(1/W) supplied by the caller (e.g. computed once on the
+// host with IEEE division, the same value): the divisions per lane and divisor are skipped.
+__device__ __forceinline__ ExactDiv exact_div_prepare_rcp(double W, double y) {
+  ExactDiv d;
+  d.W = W;
+  d.ok = (W >= 0x1p-60) && (W <= 0x1p60);
+  d.y = d.ok ? y : 1.0;
+  return d;
+}
+
+// out[i] = in[i] / W for one lane's N elements, correctly rounded, with y = RN(1/W) given.
+template <int N>
+__device__ __forceinline__ void exact_div_block_rcp(const double* in, double* out, double W, double y) {
+#if FEDAVG_FAST_DIV
+  const ExactDiv d = exact_div_prepare_rcp(W, y);
+  bool slow = !d.ok;
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = exact_div_fast(in[i], d, slow);
+  if (__builtin_expect(__ballot(slow) != 0ull, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = in[i] / W;
+  }
+#else
+  (void)y;
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = in[i] / W;
+#endif
+}
+
 // out[i] = in[i] / W for one lane's N elements, correctly rounded. The IEEE fallback runs for
 // the whole wave when any of its lanes has an element outside the fast path's range (a uniform
 // branch: the common wave executes only the fast sequence). Elements a lane does not own may

@@ -105,6 +105,7 @@ struct PArgs {
   const int32_t* exmask;      // [N][waves] bit j: the wave's receiver j skips client k (own update)
   const void* zeros;          // kChunk zero doubles (loads of absent tensors and padding)
   const double* wtot;         // [kGroup][T] per-receiver, per-segment total weight
+  const double* wrcp;         // [kGroup][T] RN(1 / wtot), IEEE division on the host
   void* const* outs;          // [kGroup][T] output pointers
   void* const* central;       // [T] centralized outputs (CENTRAL_FINAL)
   double* carry;              // flat fp64 carry of the centralized chain (P elements)
@@ -639,14 +640,16 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 #pragma unroll
   for (int j = 0; j < kJB; ++j) {
     if (j0 + j >= a.M) continue;  // (continue, not break: keeps the loop fully unrolled)
-    const double W = wtot[static_cast<int64_t>(j0 + j) * a.T + seg];
+    const int64_t wi = static_cast<int64_t>(j0 + j) * a.T + seg;
+    const double W = wtot[wi];
+    const double Wy = ((kp<double>)(a.wrcp))[wi];
     double r[kVE], s[kVE];
 #pragma unroll
     for (int v = 0; v < kVE; ++v) {
       bad_acc |= in[v] && acc[v][j] != acc[v][j];
       s[v] = acc[v][j];
     }
-    exact_div_block<kVE>(s, r, W);
+    exact_div_block_rcp<kVE>(s, r, W, Wy);
 #pragma unroll
     for (int v = 0; v < kVE; ++v) {
       acc[v][j] = r[v];
@@ -1010,7 +1013,7 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
   const size_t sz_x = align_up(sizeof(int32_t) * N * kMaxWaves, 256);
   const size_t sz_t = align_up(sizeof(double) * kGroup * T, 256);
   const size_t sz_o = align_up(sizeof(void*) * kGroup * T, 256);
-  const size_t per_g = sz_w + sz_x + sz_t + sz_o;
+  const size_t per_g = sz_w + sz_x + sz_t + sz_o + sz_t;  // ... then the reciprocals of the totals
   const size_t off_g = off_ptr + sz_ptr;
   const size_t off_c = off_g + per_g * G;
   const size_t off_z = off_c + align_up(sizeof(void*) * T, 256);
@@ -1044,6 +1047,7 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
     int32_t* hx = reinterpret_cast<int32_t*>(b + sz_w);
     double* ht = reinterpret_cast<double*>(b + sz_w + sz_x);
     void** ho = reinterpret_cast<void**>(b + sz_w + sz_x + sz_t);
+    double* hy = reinterpret_cast<double*>(b + sz_w + sz_x + sz_t + sz_o);
     const int Mg = std::min(kGroup, M - g * kGroup);
     const int waves = (Mg + kJB - 1) / kJB;
     const int wstride = kJB * waves;
@@ -1061,6 +1065,7 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
       for (int t = 0; t < T; ++t) {
         const int j = g * kGroup + r;
         ht[static_cast<size_t>(r) * T + t] = wtot[static_cast<size_t>(j) * T + t];
+        hy[static_cast<size_t>(r) * T + t] = 1.0 / wtot[static_cast<size_t>(j) * T + t];
         ho[static_cast<size_t>(r) * T + t] = out_ptrs[static_cast<int64_t>(j) * T + t];
       }
   }
@@ -1084,6 +1089,7 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
     a.exmask = reinterpret_cast<const int32_t*>(b + sz_w);
     a.wtot = reinterpret_cast<const double*>(b + sz_w + sz_x);
     a.outs = reinterpret_cast<void* const*>(b + sz_w + sz_x + sz_t);
+    a.wrcp = reinterpret_cast<const double*>(b + sz_w + sz_x + sz_t + sz_o);
     a.central = reinterpret_cast<void* const*>(p->d_blob + off_c);
     a.zeros = p->d_blob + off_z;
     a.carry = p->d_carry;

@@ -355,7 +355,7 @@ __device__ __forceinline__ void store_result(uint64_t op, int64_t start, int e, 
 // workgroup are in flight without costing registers. Each wave issues the same number of
 // DMA instructions per stage (kSC / waves clients, or all kSC when the workgroup has fewer
 // waves), waits for its own with a counted vmcnt, and one barrier per stage publishes them.
-constexpr int kSC = 4;   // clients per stage
+constexpr int kSC = 4;   // clients per stage (8 measured no faster, profiles/r04_pers_rcp_ab.txt)
 constexpr int kD = 3;    // stages in flight ahead of the one being folded
 constexpr int kRS = kD + 2;  // ring stages: the stage being written was last read two barriers ago
 
@@ -1005,8 +1005,10 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
   // skip masks, [kGroup][T] totals, [kGroup][T] outputs; then [T] centralized outputs and
   // the zero block
   const int G = (M + kGroup - 1) / kGroup;
-  const int Npad = (N + 3) / 4 * 4;  // a multiple of the register group (kU) and of a ring stage (kSC)
-  static_assert(4 % kU == 0 && 4 % kSC == 0, "padding unit");
+  // a multiple of the register group (kU) and of a ring stage (kSC), both powers of two
+  constexpr int kPad = kU > kSC ? kU : kSC;
+  static_assert((kPad & (kPad - 1)) == 0 && kPad % kU == 0 && kPad % kSC == 0, "padding unit");
+  const int Npad = (N + kPad - 1) / kPad * kPad;
   const size_t off_ptr = 0;
   const size_t sz_ptr = align_up(sizeof(void*) * T * Npad, 256);
   const size_t sz_w = align_up(sizeof(double) * Npad * kGroup, 256);

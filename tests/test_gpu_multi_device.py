@@ -328,3 +328,50 @@ def test_multi_device_c_example_reduce_in_process_rccl(hip_device, fake):
     r = subprocess.run([str(exe), "--devices", "0,0,0", "--exchange", "both"], capture_output=True, text=True,
                        timeout=180, env=env)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_round_with_quantised_and_mixed_entries(hip_device, world):
+    """Entries holding QSGD records take the separate-combine form of the peer exchange (every
+    window, their own included, into its owner's slot); dense entries fold their own window with
+    the received partials. Mixed in one round (entry 0 QSGD, the others fp32), the result is still
+    the entry-ordered composition of each entry's chain over its own (dequantised) clients."""
+    from distributed_learning_simulation_lib_amd.quantized import QSGD_F32, QuantizedTensor
+    from oracle import qsgd_oracle as qo
+
+    n = 7
+    rng = np.random.default_rng(40 + world)
+    weights = [int(w) for w in rng.integers(1, 3000, n)]
+    dense = _clients(n, torch.float32, 11)
+    recs = [[qo.quantize(c.numpy(), rng) for c in row] for row in dense]
+    deq = [[qo.dequantize(r, m, "float32") for r, m in zip(row, LAYOUT.numels)] for row in recs]
+    W = -0.0
+    for w in weights:
+        W += w
+    for mixed in (False, True):
+        m = MultiDeviceContext(LAYOUT, [0] * world)
+        try:
+            plans, rows = [], []
+            for g in range(world):
+                ks = [k for k in range(n) if _owner(k, n, world) == g]
+                t = ClientTable(LAYOUT.num_segments)
+                quant = (g == 0) or not mixed
+                for k in ks:
+                    if quant:
+                        qts = [QuantizedTensor(torch.from_numpy(r).to(hip_device), (mm,), QSGD_F32)
+                               for r, mm in zip(recs[k], LAYOUT.numels)]
+                        t.add_client([q.record for q in qts], [weights[k]] * LAYOUT.num_segments)
+                    else:
+                        t.add_client([x.to(hip_device) for x in dense[k]], [weights[k]] * LAYOUT.num_segments)
+                plans.append(m.contexts[g].plan_partial(t, QSGD_F32 if quant else torch.float32, zero_init=True))
+                rows.append([deq[k] if quant else [x.numpy() for x in dense[k]] for k in ks])
+            outs = [torch.empty(s, dtype=torch.float64, device=hip_device) for s in LAYOUT.numels]
+            for edges in ([0, m.num_tiles], chunk_edges(m.num_tiles, 3)):
+                m.round(plans, [W] * LAYOUT.num_segments, outs, torch.float64, root=world - 1, edges=edges)
+                m.raise_on_nan()
+                for s in range(LAYOUT.num_segments):
+                    shards = [[r[s] for r in rows[g]] for g in range(world)]
+                    sw = [[weights[k] for k in range(n) if _owner(k, n, world) == g] for g in range(world)]
+                    assert bits_equal(outs[s].cpu().numpy(), sharded_composition(shards, sw, W)), (mixed, edges, s)
+        finally:
+            m.close()

@@ -29,17 +29,58 @@ int dtype_code(c10::ScalarType st) {
   }
 }
 
-bool same_shape(const at::Tensor& t, PyObject* shape) {
-  if (!PyTuple_Check(shape)) return false;
-  const Py_ssize_t nd = PyTuple_GET_SIZE(shape);
-  const auto sizes = t.sizes();
-  if (static_cast<Py_ssize_t>(sizes.size()) != nd) return false;
-  for (Py_ssize_t d = 0; d < nd; ++d) {
-    const long long v = PyLong_AsLongLong(PyTuple_GET_ITEM(shape, d));
-    if (v != sizes[d]) return false;
+// The layout's shapes as native integers. A caller passes the same shapes list (one per layout,
+// never mutated) with every arrival; reading its T tuples back from Python objects cost more
+// than the rest of an arrival's checks, so the last list seen is parsed once and kept. The cache
+// holds a reference to that list (its identity cannot be reused while cached) and is only
+// touched under the GIL.
+class ShapeCache {
+ public:
+  // true when ``shapes`` is a list of tuples of ints (parsed into the cache)
+  bool load(PyObject* shapes) {
+    if (shapes == src_) return ok_;
+    Py_XDECREF(src_);
+    Py_INCREF(shapes);
+    src_ = shapes;
+    ok_ = false;
+    off_.clear();
+    dims_.clear();
+    if (!PyList_Check(shapes)) return false;
+    const Py_ssize_t T = PyList_GET_SIZE(shapes);
+    off_.reserve(T + 1);
+    for (Py_ssize_t s = 0; s < T; ++s) {
+      PyObject* sh = PyList_GET_ITEM(shapes, s);
+      off_.push_back(static_cast<int32_t>(dims_.size()));
+      if (!PyTuple_Check(sh)) return false;
+      for (Py_ssize_t d = 0; d < PyTuple_GET_SIZE(sh); ++d) {
+        const long long v = PyLong_AsLongLong(PyTuple_GET_ITEM(sh, d));
+        if (v == -1 && PyErr_Occurred()) {
+          PyErr_Clear();
+          return false;
+        }
+        dims_.push_back(v);
+      }
+    }
+    off_.push_back(static_cast<int32_t>(dims_.size()));
+    ok_ = true;
+    return true;
   }
-  return true;
-}
+  bool matches(const at::Tensor& t, int64_t seg) const {
+    const auto sizes = t.sizes();
+    const int32_t b = off_[seg], e = off_[seg + 1];
+    if (static_cast<int64_t>(sizes.size()) != e - b) return false;
+    for (int32_t d = b; d < e; ++d)
+      if (dims_[d] != sizes[d - b]) return false;
+    return true;
+  }
+
+ private:
+  PyObject* src_ = nullptr;  // deliberately never released at exit (no Python calls after finalisation)
+  bool ok_ = false;
+  std::vector<int32_t> off_;
+  std::vector<int64_t> dims_;
+};
+ShapeCache g_shapes;
 
 // stage_resident(params, index, shapes, device_index, totals, weight)
 //   params: dict name -> tensor (the update, in arrival order of its keys)
@@ -57,6 +98,7 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
     PyErr_Clear();
     return py::none();
   }
+  if (!g_shapes.load(shapes.ptr())) return py::none();
   std::vector<int64_t> ptrs(T, 0), numels(T, -1);
   std::vector<PyObject*> held(T, nullptr);
   int code = -2;  // no present tensor yet
@@ -79,7 +121,7 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
     const int c = dtype_code(t.scalar_type());
     if (c < 0 || (code != -2 && c != code)) return py::none();
     code = c;
-    if (!same_shape(t, PyList_GET_ITEM(shapes.ptr(), seg))) return py::none();
+    if (!g_shapes.matches(t, seg)) return py::none();
     ptrs[seg] = reinterpret_cast<int64_t>(t.data_ptr());
     numels[seg] = t.numel();
     held[seg] = value;
@@ -117,6 +159,7 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
 // non-contiguous tensor, a second dtype, a changed shape).
 py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_t device_index) {
   const Py_ssize_t L = PyList_GET_SIZE(shapes.ptr());
+  if (!g_shapes.load(shapes.ptr())) return py::none();
   std::vector<PyObject*> row(L, nullptr);
   int code = -2;
   PyObject *key, *value;
@@ -131,7 +174,7 @@ py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_
     const int c = dtype_code(t.scalar_type());
     if (c < 0 || (code != -2 && c != code)) return py::none();
     code = c;
-    if (!same_shape(t, PyList_GET_ITEM(shapes.ptr(), i))) return py::none();
+    if (!g_shapes.matches(t, i)) return py::none();
     row[i] = value;
   }
   if (code < 0) return py::none();
@@ -207,6 +250,11 @@ class Rows {
   Rows(int64_t T, int64_t device_index) : T_(T), dev_(device_index) {
     if (T < 1) throw std::invalid_argument("a table needs at least one segment");
   }
+  Rows(const Rows&) = delete;
+  Rows& operator=(const Rows&) = delete;
+  ~Rows() {
+    for (PyObject* o : keep_) Py_DECREF(o);  // pybind11 destroys the holder with the GIL held
+  }
 
   // append(params, index, shapes, weight, want_code) -> int
   //   >= 0: staged; the low 4 bits are the dtype code, bit 4 (16) is set when the update carried
@@ -220,13 +268,14 @@ class Rows {
       PyErr_Clear();
       return -1;
     }
-    if (PyList_GET_SIZE(shapes.ptr()) != T_) return -1;
+    if (PyList_GET_SIZE(shapes.ptr()) != T_ || !g_shapes.load(shapes.ptr())) return -1;
     const size_t base = ptrs_.size();
     ptrs_.resize(base + T_, 0);
     numels_.resize(base + T_, -1);
     uint64_t* p = ptrs_.data() + base;
     int64_t* n = numels_.data() + base;
     const size_t kbase = keep_.size();
+    keep_.reserve(kbase + T_);
     int code = -2;
     Py_ssize_t seen = 0;
     PyObject *key, *value;
@@ -234,6 +283,7 @@ class Rows {
     auto rollback = [&](int rc) {
       ptrs_.resize(base);
       numels_.resize(base);
+      for (size_t i = kbase; i < keep_.size(); ++i) Py_DECREF(keep_[i]);
       keep_.resize(kbase);
       return rc;
     };
@@ -253,10 +303,13 @@ class Rows {
       const int c = dtype_code(t.scalar_type());
       if (c < 0 || (code != -2 && c != code)) return rollback(-1);
       code = c;
-      if (!same_shape(t, PyList_GET_ITEM(shapes.ptr(), seg))) return rollback(-1);
+      if (!g_shapes.matches(t, seg)) return rollback(-1);
       p[seg] = reinterpret_cast<uint64_t>(t.data_ptr());
       n[seg] = t.numel();
-      keep_.push_back(t);
+      // the tensor's Python object keeps it alive until the table is dropped (a plain reference
+      // count, not the atomic one of an at::Tensor copy)
+      Py_INCREF(value);
+      keep_.push_back(value);
     }
     if (code < 0) return rollback(-1);
     if (want_code >= 0 && code != want_code) return rollback(-2 - code);
@@ -334,7 +387,7 @@ class Rows {
   std::vector<uint64_t> ptrs_;
   std::vector<double> weights_;
   std::vector<int64_t> numels_;
-  std::vector<at::Tensor> keep_;      // the staged tensors stay alive until the table is dropped
+  std::vector<PyObject*> keep_;       // owned references: the staged tensors outlive the table's launches
   std::vector<py::object> extra_keep_;
 };
 

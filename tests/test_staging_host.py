@@ -74,3 +74,22 @@ def test_native_rows_general_appends_and_validation():
     with pytest.raises(ValueError):
         t.add_resident_client([1, 2, 3], [1, 1, 1], [5, 6, 7], 8, 0, [])  # another element size
     assert t.num_clients == 2
+
+
+def test_shape_checks_follow_the_shapes_list_passed():
+    """The layout's shapes are parsed once per list object (csrc/staging_ext.cpp ShapeCache):
+    alternating lists, a same-numel reshape and a malformed list are each judged on the list
+    actually passed."""
+    s1, s2 = [(2, 3), (4,)], [(3, 2), (4,)]
+    idx = {"a": 0, "b": 1}
+    good = {"a": torch.ones(2, 3), "b": torch.ones(4)}
+    flipped = {"a": torch.ones(3, 2), "b": torch.ones(4)}
+    for _ in range(2):
+        assert ext.stage_resident(good, idx, s1, -1, {}, 1.0) is not None
+        assert ext.stage_resident(flipped, idx, s1, -1, {}, 1.0) is None  # same numel, other shape
+        assert ext.stage_resident(flipped, idx, s2, -1, {}, 1.0) is not None
+        assert ext.stage_resident(good, idx, s2, -1, {}, 1.0) is None
+        assert ext.stage_resident({"a": torch.ones(6)}, idx, s1, -1, {}, 1.0) is None  # other rank
+    assert ext.stage_resident(good, idx, [(2, 3), [4]], -1, {}, 1.0) is None  # not a tuple
+    assert ext.stage_resident(good, idx, [(2, 3), ("4",)], -1, {}, 1.0) is None  # not an int
+    assert ext.stage_resident(good, idx, s1, -1, {}, 1.0) is not None

@@ -122,10 +122,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.accumulate: bool = True
         self.aggregate_loss: bool = False
         self._device = torch.device(device) if device is not None else None
-        # 32: a 64-client round folds its first half while the second half is still being
-        # staged (0.81 vs 0.87 ms per device-resident 64 x ResNet-18 round), for one
-        # fp64 accumulator round trip per extra wave
-        self.wave_size = int(wave_size or os.environ.get("FEDAVG_WAVE_SIZE", 32))
+        # 64: with an update staged in ~2.6 us, folding half a 64-client round early no longer
+        # pays for the extra wave's fp64 accumulator round trip and launch ramp (0.756 vs 0.789 ms
+        # per device-resident 64 x ResNet-18 round; 32 was faster while
+        # staging took ~4 us per update)
+        self.wave_size = int(wave_size or os.environ.get("FEDAVG_WAVE_SIZE", 64))
         assert self.wave_size >= 1
         # early waves: a wave of at least ``wave_min`` staged clients is also folded when the next
         # update arrives while the GPU has finished every wave so far (0 = only full waves), so the
@@ -153,6 +154,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__has_data = False
         self.__ingest: HostIngest | None = None
         self.__result_flat: torch.Tensor | None = None
+        # (key, flat, output table, views) of the last round's result buffer (_result_buffer)
+        self.__result_pool: tuple | None = None
         self.__record_layouts: dict[tuple, ModelLayout] = {}
         # fed_avg_algorithm.py:59-62, kept with the hook's own objects (scalar weights)
         self.__host_totals: dict[str, Any] = {}
@@ -345,6 +348,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_id: int,
         worker_data: Message | None,
     ) -> bool:
+        if worker_data is not None and self._arrive_quick(worker_id, worker_data):
+            return True
         res = super().process_worker_data(worker_id, worker_data)
         if not res:
             return False
@@ -425,6 +430,45 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self._accumulate_parameter(worker_data=worker_data, name=name, parameter=parameter)
         if self.accumulate:
             self._stage_client(worker_id=worker_id)
+        return True
+
+    def _arrive_quick(self, worker_id: int, worker_data: Any) -> bool:
+        """The common arrival in one short pass: a full ParameterMessage with a number weight,
+        after the round's first arrival, into the wave's native table while it has room. The same
+        state changes as the general flow below (the message recorded (aggregation_algorithm.py:
+        93-102), its update appended to the wave (``Rows.append``), the totals += w (:59-62), the
+        payload released (:64)); False with nothing changed for anything else."""
+        table = self.__table
+        if (type(table) is not NativeClientTable or self.__round_fresh or self.__ew is not False or self.__table_delta
+                or self.__multi_devices is not None or not self.accumulate or not self.__default_hooks
+                or message_kind(worker_data) != KIND_PARAMETER):
+            return False
+        w = worker_data.aggregation_weight
+        params = worker_data.parameter
+        fast = self.__fast
+        if (type(w) not in (int, float) or type(params) is not dict or fast is None
+                or fast[0] is not self.__layout or self._wave_due(table.num_clients)):
+            return False
+        want = _STAGING_CODES.get(self.__table_dtype, -3)
+        if want == -3:
+            return False
+        rc = table.rows.append(params, fast[1], fast[2], w, want)
+        if rc < 0:
+            return False  # nothing changed: the general flow decides
+        if rc & 16 and not self.__host_totals:
+            self.__uniform_total = w if self.__uniform_count == 0 else self.__uniform_total + w
+            self.__uniform_count += 1
+        else:
+            self._materialize_totals()
+            totals = self.__host_totals
+            for name in params:
+                if name in totals:
+                    totals[name] += w
+                else:
+                    totals[name] = w
+        self._all_worker_data[worker_id] = worker_data
+        self.__has_data = True
+        worker_data.parameter = {}
         return True
 
     def _stage_natively(self, params: Any, w: Any, delta: bool = False) -> bool:
@@ -941,9 +985,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                               for i in self.__keep)
         out_dtype = torch.float64 if custom_divide else self.result_dtype
         offs, total, shapes = self._result_geometry(out_dtype)
-        flat = torch.empty(total, dtype=out_dtype, device=self.device)
+        flat, outs, views = self._result_buffer(out_dtype, reuse=not custom_divide)
         self.__result_flat = None if custom_divide else flat
-        outs = OutputTable.from_flat(flat, offs, native)
         delta = self.__table_delta and table is not None
         try:
             if self.__ew:
@@ -976,10 +1019,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             result: ModelParameter = {}
             if not custom_divide:
                 # the segments as shaped views of the flat result (one native call when the staging
-                # extension is built), made while the kernel runs
-                ext = _staging.module()
-                views = ext.views(flat, offs, shapes) if ext is not None else \
-                    [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+                # extension is built), made while the kernel runs — or the reused buffer's own
+                if views is None:
+                    views = self._result_views(flat, outs, out_dtype)
                 for j, i in enumerate(self.__keep):
                     result[layout.names[i]] = views[j]
             ctx.raise_on_nan(pending)  # the round ends on the host: :93 / :97 asserted
@@ -1032,9 +1074,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             totals = [float(self.__host_totals[layout.names[i]]) for i in self.__keep]
         out_dtype = torch.float64 if custom_divide else self.result_dtype
         offs, total, shapes = self._result_geometry(out_dtype)
-        flat = torch.empty(total, dtype=out_dtype, device=self.device)
+        flat, outs, views = self._result_buffer(out_dtype, reuse=not custom_divide)
         self.__result_flat = None if custom_divide else flat
-        outs = OutputTable.from_flat(flat, offs, native)
         try:
             m.combine(totals, outs, out_dtype, root=0, exchange=self.exchange)
         except Exception:
@@ -1043,9 +1084,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         m.raise_on_nan(pending)  # the round ends on the host: :35 / :93 / :97 asserted
         result: ModelParameter = {}
         if not custom_divide:
-            ext = _staging.module()
-            views = ext.views(flat, offs, shapes) if ext is not None else \
-                [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+            if views is None:
+                views = self._result_views(flat, outs, out_dtype)
             for j, i in enumerate(self.__keep):
                 result[layout.names[i]] = views[j]
             return result
@@ -1075,6 +1115,38 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             geo = (list(offs), int(total), [tuple(self.__layout.shapes[i]) for i in self.__keep])
             self.__result_geo = {key: geo}
         return geo
+
+    def _result_buffer(self, out_dtype: torch.dtype, reuse: bool = True) -> tuple[torch.Tensor, OutputTable, list | None]:
+        """(flat result buffer, its OutputTable, its segment views or None) for this round. The
+        reference hands out fresh tensors every round; a buffer of an earlier round is written
+        again only when nothing outside this object can still see it — no result tensor, view of
+        one or storage handle kept by the caller, no in-place change to the views
+        (``unobserved``, csrc/staging_ext.cpp) — so no caller can tell the difference. Otherwise
+        (or with ``reuse`` False) a fresh buffer; its views are made by ``_result_views``."""
+        native = self.__native_layout
+        assert native is not None
+        offs, total, shapes = self._result_geometry(out_dtype)
+        pool, ext = self.__result_pool, _staging.module()
+        if reuse and pool is not None and ext is not None and pool[0] == (native, out_dtype, self.device):
+            _, flat, outs, views = pool
+            if ext.unobserved(flat, views, offs, shapes):
+                return flat, outs, views
+        self.__result_pool = None  # the old buffer stays with whoever still holds its results
+        flat = torch.empty(total, dtype=out_dtype, device=self.device)
+        return flat, OutputTable.from_flat(flat, offs, native), None
+
+    def _result_views(self, flat: torch.Tensor, outs: OutputTable, out_dtype: torch.dtype) -> list[torch.Tensor]:
+        """The segments of a fresh result buffer as shaped views (one native call when the staging
+        extension is built); the buffer joins the pool for a later round."""
+        native = self.__native_layout
+        assert native is not None
+        offs, _, shapes = self._result_geometry(out_dtype)
+        ext = _staging.module()
+        if ext is None:
+            return [flat[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+        views = ext.views(flat, offs, shapes)
+        self.__result_pool = ((native, out_dtype, self.device), flat, outs, views)
+        return views
 
     def _total_for(self, name: str, seg: int) -> Any:
         """The total object the reference hands _apply_total_weight (fed_avg_algorithm.py:95)."""
@@ -1119,6 +1191,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self.__multi.reset()
 
     def exit(self) -> None:
+        self.__result_pool = None
         if self.__ctx is not None:
             self.__ctx.close()
             self.__ctx = None

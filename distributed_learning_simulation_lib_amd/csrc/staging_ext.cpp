@@ -31,26 +31,49 @@ int dtype_code(c10::ScalarType st) {
 
 // The layout's shapes as native integers. A caller passes the same shapes list (one per layout,
 // never mutated) with every arrival; reading its T tuples back from Python objects cost more
-// than the rest of an arrival's checks, so the last list seen is parsed once and kept. The cache
-// holds a reference to that list (its identity cannot be reused while cached) and is only
-// touched under the GIL.
+// than the rest of an arrival's checks, so the last few lists seen are parsed once and kept. The
+// cache holds a reference to each list it keeps (its identity cannot be reused while cached) and
+// is only touched under the GIL.
+struct ShapeSet {
+  PyObject* src = nullptr;  // deliberately never released at exit (no Python calls after finalisation)
+  bool ok = false;
+  std::vector<int32_t> off;
+  std::vector<int64_t> dims;
+  bool matches(const at::Tensor& t, int64_t seg) const {
+    const auto sizes = t.sizes();
+    const int32_t b = off[seg], e = off[seg + 1];
+    if (static_cast<int64_t>(sizes.size()) != e - b) return false;
+    for (int32_t d = b; d < e; ++d)
+      if (dims[d] != sizes[d - b]) return false;
+    return true;
+  }
+};
+
 class ShapeCache {
  public:
-  // true when ``shapes`` is a list of tuples of ints (parsed into the cache)
-  bool load(PyObject* shapes) {
-    if (shapes == src_) return ok_;
-    Py_XDECREF(src_);
+  // the parsed set of ``shapes`` (a list of tuples of ints), or nullptr when it is not one
+  const ShapeSet* get(PyObject* shapes) {
+    for (const ShapeSet& s : sets_)
+      if (s.src == shapes) return s.ok ? &s : nullptr;
+    ShapeSet& s = sets_[next_];
+    next_ = (next_ + 1) % kSets;
+    Py_XDECREF(s.src);
     Py_INCREF(shapes);
-    src_ = shapes;
-    ok_ = false;
-    off_.clear();
-    dims_.clear();
+    s.src = shapes;
+    s.ok = parse(shapes, s);
+    return s.ok ? &s : nullptr;
+  }
+
+ private:
+  static bool parse(PyObject* shapes, ShapeSet& s) {
+    s.off.clear();
+    s.dims.clear();
     if (!PyList_Check(shapes)) return false;
     const Py_ssize_t T = PyList_GET_SIZE(shapes);
-    off_.reserve(T + 1);
-    for (Py_ssize_t s = 0; s < T; ++s) {
-      PyObject* sh = PyList_GET_ITEM(shapes, s);
-      off_.push_back(static_cast<int32_t>(dims_.size()));
+    s.off.reserve(T + 1);
+    for (Py_ssize_t i = 0; i < T; ++i) {
+      PyObject* sh = PyList_GET_ITEM(shapes, i);
+      s.off.push_back(static_cast<int32_t>(s.dims.size()));
       if (!PyTuple_Check(sh)) return false;
       for (Py_ssize_t d = 0; d < PyTuple_GET_SIZE(sh); ++d) {
         const long long v = PyLong_AsLongLong(PyTuple_GET_ITEM(sh, d));
@@ -58,27 +81,15 @@ class ShapeCache {
           PyErr_Clear();
           return false;
         }
-        dims_.push_back(v);
+        s.dims.push_back(v);
       }
     }
-    off_.push_back(static_cast<int32_t>(dims_.size()));
-    ok_ = true;
+    s.off.push_back(static_cast<int32_t>(s.dims.size()));
     return true;
   }
-  bool matches(const at::Tensor& t, int64_t seg) const {
-    const auto sizes = t.sizes();
-    const int32_t b = off_[seg], e = off_[seg + 1];
-    if (static_cast<int64_t>(sizes.size()) != e - b) return false;
-    for (int32_t d = b; d < e; ++d)
-      if (dims_[d] != sizes[d - b]) return false;
-    return true;
-  }
-
- private:
-  PyObject* src_ = nullptr;  // deliberately never released at exit (no Python calls after finalisation)
-  bool ok_ = false;
-  std::vector<int32_t> off_;
-  std::vector<int64_t> dims_;
+  static constexpr int kSets = 4;  // the staging maps and result geometry of a layout or two
+  ShapeSet sets_[kSets];
+  int next_ = 0;
 };
 ShapeCache g_shapes;
 
@@ -98,7 +109,8 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
     PyErr_Clear();
     return py::none();
   }
-  if (!g_shapes.load(shapes.ptr())) return py::none();
+  const ShapeSet* shp = g_shapes.get(shapes.ptr());
+  if (shp == nullptr) return py::none();
   std::vector<int64_t> ptrs(T, 0), numels(T, -1);
   std::vector<PyObject*> held(T, nullptr);
   int code = -2;  // no present tensor yet
@@ -121,7 +133,7 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
     const int c = dtype_code(t.scalar_type());
     if (c < 0 || (code != -2 && c != code)) return py::none();
     code = c;
-    if (!g_shapes.matches(t, seg)) return py::none();
+    if (!shp->matches(t, seg)) return py::none();
     ptrs[seg] = reinterpret_cast<int64_t>(t.data_ptr());
     numels[seg] = t.numel();
     held[seg] = value;
@@ -159,7 +171,8 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
 // non-contiguous tensor, a second dtype, a changed shape).
 py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_t device_index) {
   const Py_ssize_t L = PyList_GET_SIZE(shapes.ptr());
-  if (!g_shapes.load(shapes.ptr())) return py::none();
+  const ShapeSet* shp = g_shapes.get(shapes.ptr());
+  if (shp == nullptr) return py::none();
   std::vector<PyObject*> row(L, nullptr);
   int code = -2;
   PyObject *key, *value;
@@ -174,7 +187,7 @@ py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_
     const int c = dtype_code(t.scalar_type());
     if (c < 0 || (code != -2 && c != code)) return py::none();
     code = c;
-    if (!g_shapes.matches(t, i)) return py::none();
+    if (!shp->matches(t, i)) return py::none();
     row[i] = value;
   }
   if (code < 0) return py::none();
@@ -206,6 +219,38 @@ py::object row_pointers(py::list row, py::list numels, int64_t device_index, int
     out[t] = py::int_(reinterpret_cast<int64_t>(v.data_ptr()));
   }
   return out;
+}
+
+// unobserved(flat, views, offsets, shapes) — true when the result buffer of an earlier round can be
+// written again without anyone seeing it change: ``views`` (made by views() below, held by the
+// caller's pool list) are the only tensors on the buffer's storage (storage use count = 1 + the
+// views), nothing else references them (the list's own reference, no C++ holder, no Python
+// attributes, no autograd state, no names) and each still has the geometry views() gave it.
+// Anything else — a result the caller kept, a view of a result, its storage object, an in-place
+// reshape — answers false and the caller allocates a fresh buffer, as every round did before.
+bool unobserved(const at::Tensor& flat, py::list views, py::list offsets, py::list shapes) {
+  const Py_ssize_t T = PyList_GET_SIZE(views.ptr());
+  const ShapeSet* shp = g_shapes.get(shapes.ptr());
+  if (shp == nullptr || PyList_GET_SIZE(shapes.ptr()) != T || PyList_GET_SIZE(offsets.ptr()) != T ||
+      !flat.has_storage() || flat.dim() != 1 || !flat.is_contiguous())
+    return false;
+  const c10::Storage& st = flat.storage();
+  if (st.use_count() != 1 + static_cast<int64_t>(T)) return false;
+  const char* base = static_cast<const char*>(st.data()) + flat.storage_offset() * flat.itemsize();
+  for (Py_ssize_t t = 0; t < T; ++t) {
+    PyObject* o = PyList_GET_ITEM(views.ptr(), t);
+    if (Py_REFCNT(o) != 1 || !THPVariable_Check(o)) return false;
+    PyObject** dict = _PyObject_GetDictPtr(o);
+    if (dict != nullptr && *dict != nullptr && PyDict_Size(*dict) != 0) return false;
+    const at::Tensor& v = THPVariable_Unpack(o);
+    if (v.use_count() != 1 || v.requires_grad() || v.has_names() || !v.is_contiguous() ||
+        v.scalar_type() != flat.scalar_type() || !v.has_storage() || !v.storage().is_alias_of(st))
+      return false;
+    const int64_t off = PyLong_AsLongLong(PyList_GET_ITEM(offsets.ptr(), t));
+    if (static_cast<const char*>(v.const_data_ptr()) != base + off * flat.itemsize()) return false;
+    if (!shp->matches(v, t)) return false;
+  }
+  return true;
 }
 
 // views(flat, offsets, shapes) — contiguous views of a flat buffer: element offsets[t], shape
@@ -268,7 +313,9 @@ class Rows {
       PyErr_Clear();
       return -1;
     }
-    if (PyList_GET_SIZE(shapes.ptr()) != T_ || !g_shapes.load(shapes.ptr())) return -1;
+    if (PyList_GET_SIZE(shapes.ptr()) != T_) return -1;
+    const ShapeSet* shp = g_shapes.get(shapes.ptr());
+    if (shp == nullptr) return -1;
     const size_t base = ptrs_.size();
     ptrs_.resize(base + T_, 0);
     numels_.resize(base + T_, -1);
@@ -303,7 +350,7 @@ class Rows {
       const int c = dtype_code(t.scalar_type());
       if (c < 0 || (code != -2 && c != code)) return rollback(-1);
       code = c;
-      if (!g_shapes.matches(t, seg)) return rollback(-1);
+      if (!shp->matches(t, seg)) return rollback(-1);
       p[seg] = reinterpret_cast<uint64_t>(t.data_ptr());
       n[seg] = t.numel();
       // the tensor's Python object keeps it alive until the table is dropped (a plain reference
@@ -410,4 +457,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("resident_row", &resident_row);
   m.def("row_pointers", &row_pointers);
   m.def("views", &views);
+  m.def("unobserved", &unobserved);
 }

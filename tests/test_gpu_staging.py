@@ -193,3 +193,44 @@ def test_common_arrivals_take_the_native_table(hip_device):
     assert algo._FedAVGAlgorithm__uniform_count == 3 and algo._FedAVGAlgorithm__host_totals == {}
     out = algo.aggregate_worker_data().parameter
     assert float(out["conv"].flatten()[0]) == 1.0
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_result_buffer_reuse_never_changes_a_kept_result(hip_device, devices):
+    """Rounds write into the previous round's result buffer only when the caller let go of every
+    result tensor (FedAVGAlgorithm._result_buffer): a kept result keeps its values, a released one
+    is reused, and every round matches the oracle bit for bit."""
+    g = torch.Generator().manual_seed(11)
+    shapes = {"conv": (8, 3, 3, 3), "fc": (10, 33), "bias": (10,)}
+    kw = {"devices": [hip_device.index or 0] * 2} if devices else {"device": hip_device}
+    algo = FedAVGAlgorithm(wave_size=2, **kw)
+
+    def one_round(seed):
+        oracle = OracleFedAvg()
+        for k in range(5):
+            p = {n: torch.randn(s, generator=g) for n, s in shapes.items()}
+            w = float(seed + k + 1)
+            algo.process_worker_data(k, ParameterMessage(parameter={n: t.to(hip_device) for n, t in p.items()},
+                                                         aggregation_weight=w))
+            oracle.process_worker_data(k, OracleMessage(parameter={n: t.numpy() for n, t in p.items()},
+                                                        aggregation_weight=w))
+        got = algo.aggregate_worker_data().parameter
+        algo.clear_worker_data()
+        want = oracle.aggregate_worker_data().parameter
+        for n, v in want.items():
+            assert bits_equal(got[n].cpu().numpy(), v), n
+        return got, want
+
+    kept, kept_want = one_round(0)
+    kept_ptr = kept["fc"].data_ptr()
+    got, _ = one_round(10)  # the kept result's buffer must not be written
+    assert got["fc"].data_ptr() != kept_ptr
+    for n, v in kept_want.items():
+        assert bits_equal(kept[n].cpu().numpy(), v), n
+    ptr = got["fc"].data_ptr()
+    del got
+    again, _ = one_round(20)  # released: its buffer is written again
+    assert again["fc"].data_ptr() == ptr
+    for n, v in kept_want.items():
+        assert bits_equal(kept[n].cpu().numpy(), v), n
+    algo.exit()

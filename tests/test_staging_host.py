@@ -93,3 +93,38 @@ def test_shape_checks_follow_the_shapes_list_passed():
     assert ext.stage_resident(good, idx, [(2, 3), [4]], -1, {}, 1.0) is None  # not a tuple
     assert ext.stage_resident(good, idx, [(2, 3), ("4",)], -1, {}, 1.0) is None  # not an int
     assert ext.stage_resident(good, idx, s1, -1, {}, 1.0) is not None
+
+
+def test_result_buffer_is_reused_only_when_nobody_can_see_it():
+    """``unobserved`` (FedAVGAlgorithm._result_buffer): a result buffer of an earlier round is
+    written again only when its views are referenced by the pool list alone, untouched."""
+    flat = torch.zeros(40, dtype=torch.float64)
+    offs, shapes = [0, 8, 24], [(2, 4), (4, 4), (3,)]
+    views = ext.views(flat, offs, shapes)
+    assert ext.unobserved(flat, views, offs, shapes)
+    kept = views[1]  # a result the caller kept
+    assert not ext.unobserved(flat, views, offs, shapes)
+    del kept
+    assert ext.unobserved(flat, views, offs, shapes)
+    row = views[0][0]  # a view of a result
+    assert not ext.unobserved(flat, views, offs, shapes)
+    del row
+    alias = flat.view(4, 10)  # another tensor on the buffer
+    assert not ext.unobserved(flat, views, offs, shapes)
+    del alias
+    assert ext.unobserved(flat, views, offs, shapes)
+    assert not ext.unobserved(flat, views, [0, 8, 25], shapes)  # not where the views are
+    assert not ext.unobserved(flat, views, offs, [(2, 4), (4, 4), (1, 3)])
+    views[2].foo = 1  # a Python attribute on a result
+    assert not ext.unobserved(flat, views, offs, shapes)
+    for make in (lambda v: v.unsqueeze_(0), lambda v: v.requires_grad_()):
+        views = ext.views(flat, offs, shapes)
+        assert ext.unobserved(flat, views, offs, shapes)
+        make(views[0])  # an in-place change of a result's metadata
+        assert not ext.unobserved(flat, views, offs, shapes)
+    # a storage handle (torch may keep its Python object for the storage's lifetime: the buffer
+    # is then never reused, which only costs a fresh allocation per round)
+    flat = torch.zeros(40, dtype=torch.float64)
+    views = ext.views(flat, offs, shapes)
+    st = views[2].untyped_storage()
+    assert not ext.unobserved(flat, views, offs, shapes)

@@ -470,7 +470,18 @@ __device__ __forceinline__ void fold_ring_split(const PArgs& a, int wave, int la
   auto enter = [&](int st) {
     if (st + kD < nst) issue(st + kD);
     const int ahead = (nst - 1 - st < kD) ? nst - 1 - st : kD;
-    wait_vmcnt(ahead * per * G::kIPC);
+    // the steady state (kD stages ahead; 1, 2 or 4 clients per wave and stage for 4+, 2-3 or 1
+    // waves) waits on an immediate count: wait_vmcnt's compare-and-branch ladder over 25 counts
+    // cost 16 % of the 4-wave integer-weight round (profiles/r04_pers_static_vmcnt_ab.txt;
+    // immediates for the last stages too measured no faster)
+    if (ahead == kD && per == 1)
+      wait_vmcnt_le<kD * G::kIPC>();
+    else if (ahead == kD && per == 2)
+      wait_vmcnt_le<2 * kD * G::kIPC>();
+    else if (ahead == kD && per == 4)
+      wait_vmcnt_le<4 * kD * G::kIPC>();
+    else
+      wait_vmcnt(ahead * per * G::kIPC);
     __builtin_amdgcn_s_barrier();
   };
   for (int st = 0; st < kD && st < nst; ++st) issue(st);

@@ -98,7 +98,14 @@ class ModelLayout:
         return offs, pos
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream_handle(device: torch.device) -> ctypes.c_void_p:
+    """torch's current stream on ``device`` (the raw handle without building a Stream object:
+    this runs on every launch)."""
+    if _raw_stream is not None and device.index is not None:
+        return ctypes.c_void_p(_raw_stream(device.index))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -65,10 +65,12 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_set_fused_fold": (c_int32, [c_void_p, c_int32]),
     "fedavg_reset": (c_int32, [c_void_p, c_void_p]),
     "fedavg_total_weights": (c_int32, [c_void_p, _PD]),
-    "fedavg_accumulate": (c_int32, [c_void_p, _PP, c_int32, _PD, c_int32, c_void_p]),
+    # the client table arguments are c_void_p: numpy / ctypes pointers or the staging extension's
+    # raw addresses (no conversion objects per launch)
+    "fedavg_accumulate": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
     "fedavg_aggregate": (
         c_int32,
-        [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_int32, c_void_p],
+        [c_void_p, c_void_p, c_int32, c_void_p, c_int32, _PP, c_int32, c_void_p],
     ),
     "fedavg_accumulate_delta": (c_int32, [c_void_p, _PP, c_int32, _PD, c_int32, _PP, c_void_p]),
     "fedavg_aggregate_delta": (

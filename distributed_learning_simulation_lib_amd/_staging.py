@@ -109,5 +109,9 @@ class NativeClientTable:
             self._arrays = (n, arrs)
         return self._arrays[1]
 
+    def addresses(self) -> tuple[int, int]:
+        """Host addresses of the pointer / weight arrays (valid until the next append)."""
+        return self.rows.ptr_addr(), self.rows.weight_addr()
+
     def elementwise_arrays(self):
         raise NotImplementedError("per-element weights need fedavg.ClientTable")

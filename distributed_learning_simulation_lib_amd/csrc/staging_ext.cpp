@@ -423,6 +423,10 @@ class Rows {
   py::bytes numel_bytes() const {
     return py::bytes(reinterpret_cast<const char*>(numels_.data()), numels_.size() * sizeof(int64_t));
   }
+  // host addresses of the [clients][segments] pointer / weight arrays, valid until the next append
+  // (what FedAvgContext hands the C ABI, without a copy into Python objects)
+  uint64_t ptr_addr() const { return reinterpret_cast<uint64_t>(ptrs_.data()); }
+  uint64_t weight_addr() const { return reinterpret_cast<uint64_t>(weights_.data()); }
   int64_t num_clients() const { return rows_; }
   int64_t num_segments() const { return T_; }
   int64_t esize() const { return esize_; }
@@ -450,6 +454,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("ptr_bytes", &Rows::ptr_bytes)
       .def("weight_bytes", &Rows::weight_bytes)
       .def("numel_bytes", &Rows::numel_bytes)
+      .def("ptr_addr", &Rows::ptr_addr)
+      .def("weight_addr", &Rows::weight_addr)
       .def_property_readonly("num_clients", &Rows::num_clients)
       .def_property_readonly("num_segments", &Rows::num_segments)
       .def_property_readonly("esize", &Rows::esize);

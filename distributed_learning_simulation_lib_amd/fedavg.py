@@ -19,6 +19,7 @@ import weakref
 from collections.abc import Mapping, Sequence
 from dataclasses import dataclass
 from functools import cached_property
+from typing import Any
 
 import numpy as np
 import torch
@@ -99,6 +100,19 @@ class ModelLayout:
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_EMPTY_ARRAYS = (np.zeros(1, np.uint64), np.zeros(1, np.float64))  # module-lifetime storage
+_EMPTY_TABLE = (_EMPTY_ARRAYS[0].ctypes.data, _EMPTY_ARRAYS[1].ctypes.data)
+
+
+def _table_args(table: ClientTable) -> tuple[Any, Any]:
+    """The client table's pointer and weight arrays as C-ABI arguments: the staging extension's
+    raw addresses when the table has them, else ctypes pointers that keep its numpy arrays alive
+    for the call."""
+    addresses = getattr(table, "addresses", None)
+    if addresses is not None:
+        return addresses()
+    p, w = table.arrays()
+    return p.ctypes.data_as(_PTR), w.ctypes.data_as(_DBL)
 
 
 def _stream_handle(device: torch.device) -> ctypes.c_void_p:
@@ -442,12 +456,9 @@ class FedAvgContext:
         self._check_table(table, in_dtype)
         if table.num_clients == 0:
             return
-        p, w = table.arrays()
+        p, w = _table_args(table)
         _native.check(
-            self._lib.fedavg_accumulate(
-                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype), w.ctypes.data_as(_DBL),
-                table.num_clients, self.stream,
-            )
+            self._lib.fedavg_accumulate(self._h, p, dtype_code(in_dtype), w, table.num_clients, self.stream)
         )
 
     def aggregate(
@@ -461,14 +472,13 @@ class FedAvgContext:
         n = 0 if table is None else table.num_clients
         if table is not None:
             self._check_table(table, in_dtype)
-            p, w = table.arrays()
+            p, w = _table_args(table)
         else:
-            p, w = np.zeros(1, np.uint64), np.zeros(1, np.float64)
+            p, w = _EMPTY_TABLE
         ot = self._out_table(outs, out_dtype)
         _native.check(
             self._lib.fedavg_aggregate(
-                self._h, p.ctypes.data_as(_PTR), dtype_code(in_dtype) if n else _native.F32,
-                w.ctypes.data_as(_DBL), n, ot, out_code(out_dtype), self.stream,
+                self._h, p, dtype_code(in_dtype) if n else _native.F32, w, n, ot, out_code(out_dtype), self.stream,
             )
         )
 

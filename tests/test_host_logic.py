@@ -211,3 +211,75 @@ def test_early_wave_policy():
     assert a._wave_due(3) and not a._wave_due(2)
     b = FedAVGAlgorithm(device="cpu", wave_size=8, wave_min=0)
     assert not b._wave_due(7) and b._wave_due(8)
+
+
+def test_quick_arrival_leaves_the_general_flows_state(monkeypatch):
+    """FedAVGAlgorithm._arrive_quick (the one-pass common arrival) changes exactly what the
+    general process_worker_data flow changes: the recorded messages, the rows handed to the
+    wave's table, the running totals (uniform while updates are complete, per name after an
+    incomplete one) and the released payloads — over full, partial and late-name updates, a
+    None message and a full wave."""
+    import torch
+
+    import distributed_learning_simulation_lib_amd.algorithm.fed_avg_algorithm as fa
+    from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMessage
+
+    class Rows:
+        def __init__(self, log):
+            self.n, self.log = 0, log
+
+        @property
+        def num_clients(self):
+            return self.n
+
+        def append(self, params, index, shapes, w, want):
+            if any(k not in index for k in params):
+                return -1  # a name the layout does not know: the general flow grows the layout
+            self.n += 1
+            self.log.append((tuple(params), w))
+            return 0 | (16 if len(params) == len(index) else 0)
+
+    def run(quick: bool):
+        log, flushed = [], []
+
+        class Table:
+            def __init__(self, T, dev):
+                self.rows = Rows(log)
+
+            @property
+            def num_clients(self):
+                return self.rows.num_clients
+
+        monkeypatch.setattr(fa, "NativeClientTable", Table)
+        a = FedAVGAlgorithm(device="cpu", wave_size=3)
+        if not quick:
+            monkeypatch.setattr(a, "_arrive_quick", lambda *args: False)
+        names = ("a", "b", "c")
+        lay = {}
+
+        def fast_maps():
+            layout = a._FedAVGAlgorithm__layout
+            if lay.get("l") is not layout:
+                lay["l"] = layout
+                lay["m"] = (layout, {n: i for i, n in enumerate(layout.names)}, [(2,)] * len(layout.names), 0)
+            return lay["m"]
+
+        monkeypatch.setattr(a, "_fast_maps", fast_maps)
+        monkeypatch.setattr(a, "_flush", lambda: (flushed.append(a._FedAVGAlgorithm__table.num_clients),
+                                                  setattr(a, "_FedAVGAlgorithm__table", None)))
+        msgs = []
+        seq = [(names, 2.0), (names, 3), (("a", "b"), 1.5), None, (names, 4.0), (names, 0.5), (names, 7)]
+        for k, item in enumerate(seq):
+            if item is None:
+                a.process_worker_data(k, None)
+                continue
+            keys, w = item
+            m = ParameterMessage(parameter={n: torch.ones(2) for n in keys}, aggregation_weight=w)
+            msgs.append(m)
+            a.process_worker_data(k, m)
+        a._materialize_totals()
+        state = (log, flushed, dict(a._FedAVGAlgorithm__host_totals), sorted(a._all_worker_data),
+                 [m.parameter for m in msgs], a._FedAVGAlgorithm__has_data)
+        return state
+
+    assert run(True) == run(False)

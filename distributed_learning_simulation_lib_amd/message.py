@@ -150,9 +150,21 @@ def message_kind(obj: Any) -> int:
     return kind
 
 
+_WIRE_CACHE: dict[tuple[type, str], type] = {}
+
+
 def wire_class(like: Any, name: str) -> type:
     """The class ``name`` ("ParameterMessage", "MultipleWorkerMessage", ...) of the wire module
-    ``like`` comes from; this package's class when ``like`` is None or its module has none."""
+    ``like`` comes from; this package's class when ``like`` is None or its module has none
+    (looked up once per message class: the plugins answer every round)."""
+    key = (type(like), name)
+    cls = _WIRE_CACHE.get(key)
+    if cls is None:
+        cls = _WIRE_CACHE[key] = _find_wire_class(like, name)
+    return cls
+
+
+def _find_wire_class(like: Any, name: str) -> type:
     if like is not None:
         for cls in type(like).__mro__:
             if cls.__name__ == name and hasattr(cls, "__dataclass_fields__"):

@@ -28,7 +28,7 @@ from .. import _native, _staging
 from ..fedavg import ModelLayout, NaNAggregationError
 from ..ingest import HostIngest
 from ..message import Message, ModelParameter, MultipleWorkerMessage, ParameterMessage, is_parameter_message, wire_class
-from ..personalized import PersonalizedContext
+from ..personalized import FlatOutputs, PersonalizedContext
 from .aggregation_algorithm import (
     AggregationAlgorithm,
     context_for,
@@ -37,6 +37,9 @@ from .aggregation_algorithm import (
     to_device_operand,
     unify_dtype,
 )
+
+
+_STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # staging_ext.cpp codes
 
 
 class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
@@ -56,6 +59,13 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         self.__ctx: PersonalizedContext | None = None
         self.__ingest: HostIngest | None = None
         self.__stage_maps: tuple | None = None  # (layout, name -> position, shapes) for staging_ext
+        # dtype codes of this round's natively staged arrivals (None once one took the general path)
+        self.__native_codes: set[int] | None = set()
+        self.__weights_memo: tuple | None = None  # (receivers, arrival ids, [M][N] weights)
+        self.__geometry: tuple | None = None  # (native layout, offsets, flat size, shapes)
+        # (key, [(buffer, views)] per receiver, (buffer, views) centralized) of the last round's
+        # result buffers, written again only while nobody outside can see them (_result_rows)
+        self.__result_pool: tuple | None = None
 
     @property
     def device(self) -> torch.device:
@@ -78,10 +88,14 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         assert is_parameter_message(worker_data)
         if self.__layout is None:
             self.__layout = ModelLayout.from_parameters(worker_data.parameter)
-        row_native = self._resident_row(worker_data.parameter)
-        if row_native is not None:
+        staged = self._resident_row(worker_data.parameter)
+        if staged is not None:
+            row_native, code = staged
             self.__arrivals.append((worker_id, worker_data, row_native))
+            if self.__native_codes is not None:
+                self.__native_codes.add(code)
             return True
+        self.__native_codes = None
         unknown = [k for k in worker_data.parameter if k not in self.__layout.names]
         if unknown:
             raise NotImplementedError(
@@ -97,10 +111,10 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         self.__arrivals.append((worker_id, worker_data, self._to_device_row(row)))
         return True
 
-    def _resident_row(self, params: Any) -> list[torch.Tensor | None] | None:
+    def _resident_row(self, params: Any) -> tuple[list[torch.Tensor | None], int] | None:
         """An update already in HBM (contiguous, one kernel dtype, the layout's names and shapes)
-        in layout order, checked in one native call (csrc/staging_ext.cpp); None: the general
-        path below (which also raises the errors)."""
+        in layout order with its dtype code, checked in one native call (csrc/staging_ext.cpp);
+        None: the general path below (which also raises the errors)."""
         ext = _staging.module()
         dev = self.device
         if ext is None or dev.type != "cuda" or not isinstance(params, dict):
@@ -113,7 +127,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         _, index, shapes = self.__stage_maps
         res = ext.resident_row(params, index, shapes,
                                dev.index if dev.index is not None else torch.cuda.current_device())
-        return None if res is None else res[0]
+        return None if res is None else (res[0], res[1])
 
     def _to_device_row(self, row: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
         assert self.__layout is not None
@@ -166,43 +180,45 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         M = len(receivers)
         out: dict[int, ModelParameter] = {j: {} for j in receivers}
         central: ModelParameter = {}
+        whole = native is not None and len(keep) == layout.num_segments
         if native is not None:
-            rows = [[row[i] for i in keep] for _, _, row in self.__arrivals]
-            present = [t for r in rows for t in r if t is not None]
-            unified, dt = unify_dtype(present)
-            it = iter(unified)
-            rows = [[None if t is None else next(it) for t in r] for r in rows]
+            codes = self.__native_codes
+            if whole and codes is not None and len(codes) == 1:
+                # every arrival staged natively in one kernel dtype, no empty tensors: the rows are
+                # already the kernel's operands
+                rows = [row for _, _, row in self.__arrivals]
+                dt = _STAGING_DTYPES[next(iter(codes))]
+            else:
+                rows = [[row[i] for i in keep] for _, _, row in self.__arrivals]
+                present = [t for r in rows for t in r if t is not None]
+                unified, dt = unify_dtype(present)
+                it = iter(unified)
+                rows = [[None if t is None else next(it) for t in r] for r in rows]
             ids = [wid for wid, _, _ in self.__arrivals]
-            weights = np.zeros((M, len(ids)), dtype=np.float64)
-            for r, j in enumerate(receivers):
-                for n, wid in enumerate(ids):
-                    weights[r, n] = float(self._worker_weights[j].get(wid, 0))  # (:36)
+            weights = self._weights(receivers, ids)
             if self.__ctx is None or self.__ctx.layout != native or self.__ctx.device != self.device:
                 if self.__ctx is not None:
                     self.__ctx.close()
                 self.__ctx = PersonalizedContext(native, self.device)
             res_dtype = self.result_dtype if self.result_dtype in (torch.float32, torch.float64) else torch.float64
-            offs, padded = native.padded_offsets(8)
-            bufs = [torch.empty(padded, dtype=res_dtype, device=self.device) for _ in receivers]
-            cbuf = torch.empty(padded, dtype=torch.float64, device=self.device)
-            # M x T result tensors, already in their shapes (one native call per receiver when the
-            # staging extension is built: ~4k views per 64-receiver ResNet-18 round)
-            ext = _staging.module()
-            if ext is not None:
-                shapes = [tuple(sh) for sh in native.shapes]
-                outs = [ext.views(b, offs, shapes) for b in bufs]
-                couts = ext.views(cbuf, offs, shapes)
-            else:
-                outs = [[b[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, native.shapes)] for b in bufs]
-                couts = [cbuf[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, native.shapes)]
+            offs, padded, shapes = self._geometry(native)
+            rows_out, cent_out = self._result_rows(native, M, res_dtype, offs, padded, shapes)
             try:
-                self.__ctx.aggregate(rows, dt, ids, weights, receivers, outs, res_dtype, couts, torch.float64)
+                self.__ctx.aggregate(rows, dt, ids, weights, receivers,
+                                     FlatOutputs([b for b, _ in rows_out], offs), res_dtype,
+                                     FlatOutputs([cent_out[0]], offs), torch.float64)
             except _native.NativeError as e:
                 if e.status == _native.ERR_STATE:
                     # every update a receiver folds lacks some tensor: the reference would leave
                     # the key out of that receiver's model; complete() the messages instead
                     raise NotImplementedError(str(e)) from e
                 raise
+            # the M x T result tensors, made while the kernel runs (one native call per receiver
+            # when the staging extension is built), or the reused buffers' own
+            outs = [v if v is not None else self._views(b, offs, shapes, native) for b, v in rows_out]
+            couts = cent_out[1] if cent_out[1] is not None else self._views(cent_out[0], offs, shapes, native)
+            self.__result_pool = ((native, res_dtype, self.device), list(zip([b for b, _ in rows_out], outs)),
+                                  (cent_out[0], couts))
             flags = self.__ctx.check()
             if flags:
                 self._raise_nan(flags, rows, dt, native, outs, receivers)
@@ -210,17 +226,74 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             for r, j in enumerate(receivers):
                 out[j].update(zip(kept_names, outs[r]))
             central.update(zip(kept_names, couts))
-        for i, name in enumerate(layout.names):
-            if i not in keep:
-                for j in receivers:
-                    out[j][name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
-                central[name] = torch.empty(layout.shapes[i], dtype=torch.float64, device=self.device)
-        ordered = {j: {n: out[j][n] for n in layout.names} for j in receivers}
-        central = {n: central[n] for n in layout.names}
+        if whole:
+            ordered, central_ordered = out, central  # already every name, in layout order
+        else:
+            for i, name in enumerate(layout.names):
+                if i not in keep:
+                    for j in receivers:
+                        out[j][name] = torch.empty(layout.shapes[i], dtype=self.result_dtype, device=self.device)
+                    central[name] = torch.empty(layout.shapes[i], dtype=torch.float64, device=self.device)
+            ordered = {j: {n: out[j][n] for n in layout.names} for j in receivers}
+            central_ordered = {n: central[n] for n in layout.names}
         if self.result_device is not None:
             ordered = {j: {k: v.to(self.result_device) for k, v in p.items()} for j, p in ordered.items()}
-            central = {k: v.to(self.result_device) for k, v in central.items()}
-        return ordered, central
+            central_ordered = {k: v.to(self.result_device) for k, v in central_ordered.items()}
+        return ordered, central_ordered
+
+    def _geometry(self, native: ModelLayout) -> tuple[list[int], int, list[tuple[int, ...]]]:
+        """(element offsets, flat size, shapes) of a result buffer, one set of objects per layout
+        (the staging extension parses a shapes list once per list object)."""
+        memo = self.__geometry
+        if memo is None or memo[0] is not native:
+            offs, padded = native.padded_offsets(8)
+            memo = self.__geometry = (native, list(offs), int(padded), [tuple(sh) for sh in native.shapes])
+        return memo[1], memo[2], memo[3]
+
+    def _weights(self, receivers: list[int], ids: list[int]) -> np.ndarray:
+        """weights[r][n] = worker_weights[receiver r].get(arrival n's worker, 0) (:36); the
+        matrix of the last (receivers, arrival order) is kept (the weights are set once)."""
+        key = (tuple(receivers), tuple(ids))
+        memo = self.__weights_memo
+        if memo is not None and memo[0] == key:
+            return memo[1]
+        weights = np.zeros((len(receivers), len(ids)), dtype=np.float64)
+        for r, j in enumerate(receivers):
+            wj = self._worker_weights[j]
+            for n, wid in enumerate(ids):
+                weights[r, n] = float(wj.get(wid, 0))
+        self.__weights_memo = (key, weights)
+        return weights
+
+    @staticmethod
+    def _views(buf: torch.Tensor, offs, shapes, native: ModelLayout) -> list[torch.Tensor]:
+        ext = _staging.module()
+        if ext is not None:
+            return ext.views(buf, offs, shapes)
+        return [buf[o : o + n].view(sh) for o, n, sh in zip(offs, native.numels, shapes)]
+
+    def _result_rows(self, native: ModelLayout, M: int, res_dtype: torch.dtype, offs, padded: int, shapes):
+        """(buffer, views or None) per receiver and for the centralized model. A buffer of the
+        last round is written again only when nothing outside this object can see it (``unobserved``,
+        csrc/staging_ext.cpp: its views referenced by the pool alone, nothing else on its storage,
+        geometry untouched) — the caller cannot tell it from a fresh one; otherwise a new buffer."""
+        ext = _staging.module()
+        pool, self.__result_pool = self.__result_pool, None
+        old_rows: list = []
+        old_cent = None
+        if pool is not None and ext is not None and pool[0] == (native, res_dtype, self.device):
+            old_rows, old_cent = pool[1], pool[2]
+        rows = []
+        for r in range(M):
+            if r < len(old_rows) and ext.unobserved(old_rows[r][0], old_rows[r][1], offs, shapes):
+                rows.append(old_rows[r])
+            else:
+                rows.append((torch.empty(padded, dtype=res_dtype, device=self.device), None))
+        if old_cent is not None and ext.unobserved(old_cent[0], old_cent[1], offs, shapes):
+            cent = old_cent
+        else:
+            cent = (torch.empty(padded, dtype=torch.float64, device=self.device), None)
+        return rows, cent
 
     def _raise_nan(self, flags: int, rows, dt, native: ModelLayout, outs, receivers) -> None:
         """Map the fused flags onto the reference's assertions (error path only)."""
@@ -256,8 +329,10 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
     def clear_worker_data(self) -> None:
         super().clear_worker_data()
         self.__arrivals = []
+        self.__native_codes = set()
 
     def exit(self) -> None:
+        self.__result_pool = None
         if self.__ctx is not None:
             self.__ctx.close()
             self.__ctx = None

@@ -27,6 +27,17 @@ _I64 = ctypes.POINTER(ctypes.c_int64)
 
 
 @dataclass(frozen=True)
+class FlatOutputs:
+    """Output rows as flat contiguous buffers, one per receiver (or one for the centralized
+    model): segment t of row r starts at element ``offsets[t]`` of ``buffers[r]``. The table takes
+    the pointers from the buffers' addresses — no tensor per segment is needed before the
+    launch, so the per-segment result views can be made while the kernel runs."""
+
+    buffers: Sequence[torch.Tensor]
+    offsets: Sequence[int]
+
+
+@dataclass(frozen=True)
 class PersonalizedTables:
     """Validated device pointers of one round's clients and outputs (C-ABI arrays)."""
 
@@ -83,9 +94,9 @@ class PersonalizedContext:
         self,
         clients: Sequence[Sequence[torch.Tensor | None]],
         in_dtype: torch.dtype,
-        outs: Sequence[Sequence[torch.Tensor]],
+        outs: Sequence[Sequence[torch.Tensor]] | FlatOutputs,
         out_dtype: torch.dtype,
-        central: Sequence[torch.Tensor] | None = None,
+        central: Sequence[torch.Tensor] | FlatOutputs | None = None,
         central_dtype: torch.dtype = torch.float64,
     ) -> PersonalizedTables:
         """Validate the tensors of a round once (persistent client / output slots reuse it)."""
@@ -116,7 +127,13 @@ class PersonalizedContext:
                     raise ValueError("client tensors must be contiguous, on the device, of the input dtype and size")
                 ptrs[k * T + t] = x.data_ptr()
                 keep.append(x)
-        optrs = np.zeros(len(outs) * T, dtype=np.uint64)
+        n_recv = len(outs.buffers) if isinstance(outs, FlatOutputs) else len(outs)
+        if isinstance(outs, FlatOutputs):
+            optrs = self._flat_pointers(outs, out_dtype)
+            keep.append(outs)
+            outs = ()
+        else:
+            optrs = np.zeros(len(outs) * T, dtype=np.uint64)
         for j, row in enumerate(outs):
             got = ext.row_pointers(list(row), numels, dev_idx, out_code_) if ext is not None and len(row) == T else None
             if got is not None:
@@ -129,7 +146,13 @@ class PersonalizedContext:
                 optrs[j * T + t] = o.data_ptr()
                 keep.append(o)
         cptrs = None
-        if central is not None:
+        if isinstance(central, FlatOutputs):
+            if len(central.buffers) != 1:
+                raise ValueError("the centralized model is one flat buffer")
+            cptrs = self._flat_pointers(central, central_dtype)
+            keep.append(central)
+            central = None
+        elif central is not None:
             cptrs = np.zeros(T, dtype=np.uint64)
             got = ext.row_pointers(list(central), numels, dev_idx, c_code) if ext is not None and len(central) == T \
                 else None
@@ -141,8 +164,27 @@ class PersonalizedContext:
             if got is not None:
                 cptrs[:] = got
                 keep.append(central)
-        return PersonalizedTables(len(clients), len(outs), in_dtype, out_dtype, central_dtype, ptrs, optrs, cptrs,
+        return PersonalizedTables(len(clients), n_recv, in_dtype, out_dtype, central_dtype, ptrs, optrs, cptrs,
                                   tuple(keep))
+
+    def _flat_pointers(self, flat: FlatOutputs, dtype: torch.dtype) -> np.ndarray:
+        """[rows][T] segment pointers of flat output buffers (each checked: contiguous, 1-D, on the
+        device, of ``dtype``, holding every segment)."""
+        T = self.layout.num_segments
+        offs = np.asarray(flat.offsets, dtype=np.int64)
+        if offs.shape != (T,) or (T and offs.min() < 0):
+            raise ValueError("one non-negative element offset per segment is required")
+        need = int((offs + np.asarray(self.layout.numels, dtype=np.int64)).max()) if T else 0
+        bases = []
+        for b in flat.buffers:
+            if (b.device != self.device or b.dtype != dtype or b.dim() != 1 or not b.is_contiguous()
+                    or b.numel() < need):
+                raise ValueError("flat outputs must be contiguous 1-D buffers on the device, of the output "
+                                 "dtype, holding every segment")
+            bases.append(b.data_ptr())
+        esize = torch.empty((), dtype=dtype).element_size()
+        return (np.asarray(bases, dtype=np.uint64)[:, None]
+                + (offs.astype(np.uint64) * np.uint64(esize))[None, :]).reshape(-1)
 
     def aggregate(
         self,
@@ -151,9 +193,9 @@ class PersonalizedContext:
         client_ids: Sequence[int],
         weights: np.ndarray,
         receiver_ids: Sequence[int],
-        outs: Sequence[Sequence[torch.Tensor]] | None = None,
+        outs: Sequence[Sequence[torch.Tensor]] | FlatOutputs | None = None,
         out_dtype: torch.dtype = torch.float64,
-        central: Sequence[torch.Tensor] | None = None,
+        central: Sequence[torch.Tensor] | FlatOutputs | None = None,
         central_dtype: torch.dtype = torch.float64,
     ) -> None:
         """clients[N][T] (None = tensor not sent) or prepared tables, weights[M][N] float64."""

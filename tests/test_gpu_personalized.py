@@ -187,3 +187,38 @@ def test_personalized_with_foreign_messages(hip_device, name):
         for k, want in case.expected[r["worker_id"]].items():
             assert bits_equal(got.parameter[k].cpu().numpy(), want), f"{name}/{r['worker_id']}/{k}"
 
+
+
+def test_result_buffers_reused_only_when_unobserved(hip_device):
+    """One algorithm over three rounds: a receiver's result buffer of an earlier round is written
+    again only when the caller kept nothing of it (PersonalizedFedAVGAlgorithm._result_rows):
+    kept results keep their values, released buffers are reused, every round matches the oracle."""
+    n = 8
+    _, ww = _random_round(n, range(n), SHAPES, 7)
+    algo = PersonalizedFedAVGAlgorithm(device=hip_device)
+    algo.set_worker_weights({j: dict(v) for j, v in ww.items()})
+
+    def one_round(seed):
+        clients, _ = _random_round(n, range(n), SHAPES, seed)
+        for k, p in enumerate(clients):
+            algo.process_worker_data(k, ParameterMessage(parameter={m: t.to(hip_device) for m, t in p.items()}))
+        res = algo.aggregate_worker_data()
+        algo.clear_worker_data()
+        want = _oracle(clients, ww)
+        _assert_same(res, want)
+        return res, want
+
+    kept, kept_want = one_round(1)
+    ptr = kept.worker_data[3].parameter["fc"].data_ptr()
+    res2, want2 = one_round(2)  # everything of round 1 is still held: fresh buffers
+    assert res2.worker_data[3].parameter["fc"].data_ptr() != ptr
+    _assert_same(kept, kept_want)
+    ptr2 = res2.worker_data[3].parameter["fc"].data_ptr()
+    conv5 = res2.worker_data[5].parameter["conv"]  # one tensor of one receiver kept
+    del res2
+    res3, _ = one_round(3)
+    assert res3.worker_data[3].parameter["fc"].data_ptr() == ptr2  # released: written again
+    assert res3.worker_data[5].parameter["conv"].data_ptr() != conv5.data_ptr()
+    assert bits_equal(conv5.cpu().numpy(), want2.worker_data[5].parameter["conv"])
+    _assert_same(kept, kept_want)
+    algo.exit()

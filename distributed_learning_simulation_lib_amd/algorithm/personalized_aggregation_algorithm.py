@@ -151,19 +151,28 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             assert folded[j], f"receiver {j} received no update"
         layout = self.__layout
         assert layout is not None
-        parameters, central = self._reduce(receivers)
+        msgs_of: dict[int, list[Message]] = {}
+
+        def receivers_messages() -> None:
+            # the receiver's FedAVGAlgorithm keeps _all_worker_data[worker_id] = update: a worker
+            # that reported twice keeps its first position and its last message (built while the
+            # kernel runs)
+            for j in receivers:
+                by_id: dict[int, Message] = {}
+                for n in folded[j]:
+                    by_id[self.__arrivals[n][0]] = self.__arrivals[n][1]
+                msgs_of[j] = list(by_id.values())
+
+        parameters, central = self._reduce(receivers, under_kernel=receivers_messages)
+        if not msgs_of:
+            receivers_messages()
         # answer in the caller's wire classes (the reference server matches
         # `case MultipleWorkerMessage()`, aggregation_server.py:84-86)
         like = self.__arrivals[0][1] if self.__arrivals else None
         param_cls = wire_class(like, "ParameterMessage")
         results: dict[int, ParameterMessage] = {}
         for j in receivers:
-            # the receiver's FedAVGAlgorithm keeps _all_worker_data[worker_id] = update: a worker
-            # that reported twice keeps its first position and its last message
-            by_id: dict[int, Message] = {}
-            for n in folded[j]:
-                by_id[self.__arrivals[n][0]] = self.__arrivals[n][1]
-            msgs = list(by_id.values())
+            msgs = msgs_of[j]
             results[j] = param_cls(
                 parameter=parameters[j],
                 end_training=msgs[0].end_training,
@@ -173,7 +182,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         return wire_class(like, "MultipleWorkerMessage")(worker_data=results,
                                                          other_data={"centralized_parameter": central})
 
-    def _reduce(self, receivers: list[int]) -> tuple[dict[int, ModelParameter], ModelParameter]:
+    def _reduce(self, receivers: list[int], under_kernel: Any = None) -> tuple[dict[int, ModelParameter], ModelParameter]:
         layout = self.__layout
         assert layout is not None
         native, keep = split_empty(layout)
@@ -219,13 +228,15 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             couts = cent_out[1] if cent_out[1] is not None else self._views(cent_out[0], offs, shapes, native)
             self.__result_pool = ((native, res_dtype, self.device), list(zip([b for b, _ in rows_out], outs)),
                                   (cent_out[0], couts))
-            flags = self.__ctx.check()
-            if flags:
-                self._raise_nan(flags, rows, dt, native, outs, receivers)
             kept_names = [layout.names[i] for i in keep]
             for r, j in enumerate(receivers):
                 out[j].update(zip(kept_names, outs[r]))
             central.update(zip(kept_names, couts))
+            if under_kernel is not None:
+                under_kernel()  # the caller's host work that needs no result values
+            flags = self.__ctx.check()
+            if flags:
+                self._raise_nan(flags, rows, dt, native, outs, receivers)
         if whole:
             ordered, central_ordered = out, central  # already every name, in layout order
         else:

@@ -171,13 +171,15 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         like = self.__arrivals[0][1] if self.__arrivals else None
         param_cls = wire_class(like, "ParameterMessage")
         results: dict[int, ParameterMessage] = {}
+        # no arrival carries other_data: every receiver's merge is an empty dict (:136-149)
+        no_other = all(not getattr(m, "other_data", None) for _, m, _ in self.__arrivals)
         for j in receivers:
             msgs = msgs_of[j]
             results[j] = param_cls(
                 parameter=parameters[j],
                 end_training=msgs[0].end_training,
                 in_round=msgs[0].in_round,
-                other_data=self._check_and_reduce_other_data(msgs),
+                other_data={} if no_other else self._check_and_reduce_other_data(msgs),
             )
         return wire_class(like, "MultipleWorkerMessage")(worker_data=results,
                                                          other_data={"centralized_parameter": central})

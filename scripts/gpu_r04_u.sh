@@ -15,4 +15,7 @@ timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_defa
 for a in "--workload plugin" "--workload gradient" "--workload personalized --pers-weights int" "--workload personalized --pers-weights float"; do
   timeout -k 10 300 python bench.py $a --no-cpu-baseline --no-probe --steps 20 --warmup 5 >> $O/lines.jsonl 2>> $O/lines.err || { echo "bench $a failed"; tail -20 $O/lines.err; exit 1; }
 done
+
+timeout -k 10 300 python scripts/plugin_pers_bench.py > $O/plugin_pers.txt 2>&1 || { tail -30 $O/plugin_pers.txt; exit 1; }
+sed -n 2p $O/plugin_pers.txt
 echo done

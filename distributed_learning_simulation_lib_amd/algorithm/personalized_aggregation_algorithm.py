@@ -61,6 +61,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         self.__stage_maps: tuple | None = None  # (layout, name -> position, shapes) for staging_ext
         # dtype codes of this round's natively staged arrivals (None once one took the general path)
         self.__native_codes: set[int] | None = set()
+        self.__ptr_rows: list[bytes] = []  # the natively staged arrivals' device addresses
         self.__weights_memo: tuple | None = None  # (receivers, arrival ids, [M][N] weights)
         self.__geometry: tuple | None = None  # (native layout, offsets, flat size, shapes)
         # (key, [(buffer, views)] per receiver, (buffer, views) centralized) of the last round's
@@ -90,10 +91,11 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             self.__layout = ModelLayout.from_parameters(worker_data.parameter)
         staged = self._resident_row(worker_data.parameter)
         if staged is not None:
-            row_native, code = staged
+            row_native, code, ptr_row = staged
             self.__arrivals.append((worker_id, worker_data, row_native))
             if self.__native_codes is not None:
                 self.__native_codes.add(code)
+                self.__ptr_rows.append(ptr_row)
             return True
         self.__native_codes = None
         unknown = [k for k in worker_data.parameter if k not in self.__layout.names]
@@ -111,10 +113,10 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         self.__arrivals.append((worker_id, worker_data, self._to_device_row(row)))
         return True
 
-    def _resident_row(self, params: Any) -> tuple[list[torch.Tensor | None], int] | None:
+    def _resident_row(self, params: Any) -> tuple[list[torch.Tensor | None], int, bytes] | None:
         """An update already in HBM (contiguous, one kernel dtype, the layout's names and shapes)
-        in layout order with its dtype code, checked in one native call (csrc/staging_ext.cpp);
-        None: the general path below (which also raises the errors)."""
+        in layout order with its dtype code and device addresses, checked in one native call
+        (csrc/staging_ext.cpp); None: the general path below (which also raises the errors)."""
         ext = _staging.module()
         dev = self.device
         if ext is None or dev.type != "cuda" or not isinstance(params, dict):
@@ -127,7 +129,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         _, index, shapes = self.__stage_maps
         res = ext.resident_row(params, index, shapes,
                                dev.index if dev.index is not None else torch.cuda.current_device())
-        return None if res is None else (res[0], res[1])
+        return None if res is None else (res[0], res[1], res[2])
 
     def _to_device_row(self, row: list[torch.Tensor | None]) -> list[torch.Tensor | None]:
         assert self.__layout is not None
@@ -194,11 +196,13 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         whole = native is not None and len(keep) == layout.num_segments
         if native is not None:
             codes = self.__native_codes
+            client_ptrs = None
             if whole and codes is not None and len(codes) == 1:
                 # every arrival staged natively in one kernel dtype, no empty tensors: the rows are
-                # already the kernel's operands
+                # already the kernel's operands, checked and addressed at arrival
                 rows = [row for _, _, row in self.__arrivals]
                 dt = _STAGING_DTYPES[next(iter(codes))]
+                client_ptrs = b"".join(self.__ptr_rows)
             else:
                 rows = [[row[i] for i in keep] for _, _, row in self.__arrivals]
                 present = [t for r in rows for t in r if t is not None]
@@ -217,7 +221,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
             try:
                 self.__ctx.aggregate(rows, dt, ids, weights, receivers,
                                      FlatOutputs([b for b, _ in rows_out], offs), res_dtype,
-                                     FlatOutputs([cent_out[0]], offs), torch.float64)
+                                     FlatOutputs([cent_out[0]], offs), torch.float64, client_ptrs)
             except _native.NativeError as e:
                 if e.status == _native.ERR_STATE:
                     # every update a receiver folds lacks some tensor: the reference would leave
@@ -343,6 +347,7 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         super().clear_worker_data()
         self.__arrivals = []
         self.__native_codes = set()
+        self.__ptr_rows = []
 
     def exit(self) -> None:
         self.__result_pool = None

@@ -166,7 +166,8 @@ py::object stage_resident(py::dict params, py::dict index, py::list shapes, int6
 // resident_row(params, index, shapes, device_index) — PersonalizedFedAVG's arrival staging
 // (personalized_aggregation_algorithm.py:23-43 keeps the update; the kernel reads it in place):
 //   index: dict name -> layout position, shapes: list of the layout's shapes (tuples)
-// Returns (row, dtype_code): the update's tensors in layout order (None where absent), or None
+// Returns (row, dtype_code, pointers): the update's tensors in layout order (None where absent)
+// and their device addresses (uint64 bytes, 0 where absent), or None
 // when anything needs the general path (an unknown name, a host tensor, another device, a
 // non-contiguous tensor, a second dtype, a changed shape).
 py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_t device_index) {
@@ -174,6 +175,7 @@ py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_
   const ShapeSet* shp = g_shapes.get(shapes.ptr());
   if (shp == nullptr) return py::none();
   std::vector<PyObject*> row(L, nullptr);
+  std::vector<uint64_t> ptrs(L, 0);
   int code = -2;
   PyObject *key, *value;
   Py_ssize_t pos = 0;
@@ -189,12 +191,14 @@ py::object resident_row(py::dict params, py::dict index, py::list shapes, int64_
     code = c;
     if (!shp->matches(t, i)) return py::none();
     row[i] = value;
+    ptrs[i] = reinterpret_cast<uint64_t>(t.data_ptr());
   }
   if (code < 0) return py::none();
   py::list out(L);
   for (Py_ssize_t i = 0; i < L; ++i)
     out[i] = row[i] ? py::reinterpret_borrow<py::object>(row[i]) : py::none();
-  return py::make_tuple(out, code);
+  return py::make_tuple(out, code,
+                        py::bytes(reinterpret_cast<const char*>(ptrs.data()), ptrs.size() * sizeof(uint64_t)));
 }
 
 // row_pointers(row, numels, device_index, dtype_code) — the validation + pointer pass of a client

@@ -98,12 +98,24 @@ class PersonalizedContext:
         out_dtype: torch.dtype,
         central: Sequence[torch.Tensor] | FlatOutputs | None = None,
         central_dtype: torch.dtype = torch.float64,
+        client_ptrs: bytes | None = None,
     ) -> PersonalizedTables:
-        """Validate the tensors of a round once (persistent client / output slots reuse it)."""
+        """Validate the tensors of a round once (persistent client / output slots reuse it).
+        ``client_ptrs``: the rows' device addresses ([N][T] uint64) when the caller already checked
+        every client tensor against the layout and ``in_dtype`` (the staging extension's
+        ``resident_row``); the rows are then only kept alive, not walked again."""
         T = self.layout.num_segments
         numels = self.layout.numels
-        ptrs = np.zeros(len(clients) * T, dtype=np.uint64)
         keep: list = []
+        if client_ptrs is not None:
+            ptrs = np.frombuffer(client_ptrs, dtype=np.uint64)
+            if ptrs.size != len(clients) * T:
+                raise ValueError("client pointer rows do not match the clients and the layout")
+            keep.append(clients)
+            clients_to_walk: Sequence = ()
+        else:
+            ptrs = np.zeros(len(clients) * T, dtype=np.uint64)
+            clients_to_walk = clients
         # the checks + pointer pass of a row in one native call (csrc/staging_ext.cpp) when built;
         # a row it refuses goes through the loop below, which names the offending tensor
         ext = _staging.module() if self.device.type == "cuda" else None
@@ -112,7 +124,7 @@ class PersonalizedContext:
             dev_idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         in_code, out_code_, c_code = (_STAGING_CODES.get(in_dtype, -9), _STAGING_CODES.get(out_dtype, -9),
                                       _STAGING_CODES.get(central_dtype, -9))
-        for k, row in enumerate(clients):
+        for k, row in enumerate(clients_to_walk):
             if len(row) != T:
                 raise ValueError("client row does not match the layout")
             got = ext.row_pointers(list(row), numels, dev_idx, in_code) if ext is not None else None
@@ -197,10 +209,12 @@ class PersonalizedContext:
         out_dtype: torch.dtype = torch.float64,
         central: Sequence[torch.Tensor] | FlatOutputs | None = None,
         central_dtype: torch.dtype = torch.float64,
+        client_ptrs: bytes | None = None,
     ) -> None:
-        """clients[N][T] (None = tensor not sent) or prepared tables, weights[M][N] float64."""
+        """clients[N][T] (None = tensor not sent) or prepared tables, weights[M][N] float64
+        (``client_ptrs``: see ``tables``)."""
         tab = clients if isinstance(clients, PersonalizedTables) else \
-            self.tables(clients, in_dtype, outs or (), out_dtype, central, central_dtype)
+            self.tables(clients, in_dtype, outs or (), out_dtype, central, central_dtype, client_ptrs)
         N, M = tab.num_clients, len(receiver_ids)
         w = np.ascontiguousarray(weights, dtype=np.float64)
         if w.shape != (M, N) or len(client_ids) != N or tab.num_receivers != M:

@@ -811,7 +811,7 @@ struct fedavg_pers {
   hipEvent_t blob_done = nullptr;
   bool blob_used = false;
   bool allow_fma = true;
-  bool ring = true;  // FEDAVG_PERS_RING=0: the fused fold of whole chunks takes the register pipeline too (A/B)
+  bool ring = false;  // FEDAVG_PERS_RING=1: the fused fold of whole fp32 / fp64 chunks streams through the LDS ring
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
 };
@@ -1127,9 +1127,10 @@ int32_t fedavg_pers_aggregate(fedavg_pers* p, const void* const* client_ptrs, in
       PERS_HIP_TRY(hipEventCreate(&e1));
       PERS_HIP_TRY(hipEventRecord(e0, s));
     }
-    // the LDS ring (whole aligned fp32 / fp64 chunks) for the fused fold: measured 3.08 -> 2.85 ms
-    // (64 x 64 ResNet-18); the mul + add fold is VALU-bound and ~3 % faster on the register
-    // pipeline, which every other case keeps
+    // the LDS ring (whole aligned fp32 / fp64 chunks, fused fold only) is opt-in: with round 4's
+    // register pipeline (split weight halves, incremental rows) the integer-weight round runs
+    // 2.78 ms median (2.74-2.99) there against 2.89-3.40 ms medians (2.71-3.43) on the ring,
+    // interleaved on one box (profiles/r04_pers_ring_vs_regs.txt)
     a.ring = p->ring && fold == PF_FMA && (in_dtype == FEDAVG_F32 || in_dtype == FEDAVG_F64);
     const size_t slice = static_cast<size_t>(kChunk) * (in_dtype == FEDAVG_F64 ? 8 : 4);
     const size_t lds = sizeof(double) * 64 * kVE +

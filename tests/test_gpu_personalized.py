@@ -129,10 +129,13 @@ def test_random_round_matches_oracle(hip_device, weight_kind):
     _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))
 
 
+@pytest.mark.parametrize("ring", ["1", "0"])
 @pytest.mark.parametrize("receivers", [40, 72, 100, 120])
-def test_int_weights_ring_with_uneven_wave_counts(hip_device, receivers):
-    # integer weights take the LDS-DMA client ring on whole aligned fp32 chunks; 3 / 5 / 7 / 8
-    # waves of 16 receivers split a ring stage of 4 clients unevenly (or not at all) between waves
+def test_int_weights_ring_with_uneven_wave_counts(hip_device, receivers, ring, monkeypatch):
+    # integer weights with FEDAVG_PERS_RING=1 take the LDS-DMA client ring on whole aligned fp32
+    # chunks; 3 / 5 / 7 / 8 waves of 16 receivers split a ring stage of 4 clients unevenly (or not
+    # at all) between waves; "0" is the default register pipeline
+    monkeypatch.setenv("FEDAVG_PERS_RING", ring)  # read when the native context is created
     clients, ww = _random_round(receivers, range(receivers), {"a": (1024,), "b": (300,)}, 110 + receivers,
                                 weight_kind="int")
     _assert_same(_hip(clients, ww, hip_device), _oracle(clients, ww))

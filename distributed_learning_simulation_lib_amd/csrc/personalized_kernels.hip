@@ -716,7 +716,9 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
   }
 }
 
-template <typename T, int FOLD>
+// RING: the fused fold of whole aligned fp32 / fp64 chunks streams through the LDS ring (opt-in,
+// its own instantiation so the default register pipeline's allocation is its own)
+template <typename T, int FOLD, bool RING = false>
 // three waves per SIMD (<= 168 VGPRs): the fold hides its load latency across waves
 __global__ __launch_bounds__(64 * kMaxWaves) __attribute__((amdgpu_waves_per_eu(3))) void personalized_kernel(PArgs a) {
   // dynamic LDS: the centralized chain (64 x kVE doubles), then the client ring (fp32 / fp64)
@@ -730,13 +732,11 @@ __global__ __launch_bounds__(64 * kMaxWaves) __attribute__((amdgpu_waves_per_eu(
   const int count = cd[1];
   const int64_t start = ((kp<int64_t>)(a.chunks + blockIdx.x))[1];
   if (count == kChunk && a.aligned) {
-    if constexpr (kHasGlds<T> && FOLD == PF_FMA) {  // the host enables the ring for the fused fold only
-      if (a.ring) {
-        pers_body<T, FOLD, true, true>(a, wave, lane, seg, count, start, chain, ring);
-        return;
-      }
+    if constexpr (RING && kHasGlds<T> && FOLD == PF_FMA) {
+      pers_body<T, FOLD, true, true>(a, wave, lane, seg, count, start, chain, ring);
+    } else {
+      pers_body<T, FOLD, true, false>(a, wave, lane, seg, count, start, chain, ring);
     }
-    pers_body<T, FOLD, true, false>(a, wave, lane, seg, count, start, chain, ring);
   } else {
     pers_body<T, FOLD, false, false>(a, wave, lane, seg, count, start, chain, ring);
   }
@@ -821,6 +821,12 @@ namespace {
 template <typename T>
 hipError_t launch_pers_t(const PArgs& a, int fold, int nchunks, int threads, size_t lds, hipStream_t s) {
   if (fold == PF_FMA) {
+    if constexpr (kHasGlds<T>) {
+      if (a.ring) {
+        hipLaunchKernelGGL((personalized_kernel<T, PF_FMA, true>), dim3(nchunks), dim3(threads), lds, s, a);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((personalized_kernel<T, PF_FMA>), dim3(nchunks), dim3(threads), lds, s, a);
   } else {
     hipLaunchKernelGGL((personalized_kernel<T, PF_MULADD>), dim3(nchunks), dim3(threads), lds, s, a);

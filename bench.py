@@ -90,23 +90,83 @@ def _launch_ranks(argv: list[str]) -> int | None:
     pre = argparse.ArgumentParser(add_help=False)
     pre.add_argument("--gpus", type=int, default=1)
     pre.add_argument("--launch-timeout", type=float, default=480.0)
+    pre.add_argument("--one-process-timeout", type=float, default=200.0)
     pre.add_argument("--comm", default="native")
     pre.add_argument("--no-fallback", action="store_true")
     pre.add_argument("--procs", type=int, default=0)
+    pre.add_argument("--workload", default="fedavg")
+    pre.add_argument("--shard", default="clients")
     known, _ = pre.parse_known_args(argv)
     if known.gpus <= 1 or "WORLD_SIZE" in os.environ or known.procs == 1:
         return None
     deadline = time.monotonic() + known.launch_timeout
     status_dir = tempfile.mkdtemp(prefix="bench_status_")
-    rc, failed = _run_ranks(argv, known.gpus, deadline, known.launch_timeout, status_dir, None)
+    note = None
+    if known.procs == 0 and known.workload == "fedavg" and known.shard == "clients":
+        # the default: ONE process drives the N GPUs (the peer-window exchange) —
+        # the reference's single server process (simulation_lib/server/server.py:122-152)
+        budget = min(known.one_process_timeout, known.launch_timeout / 2)
+        rc, why = _run_one_process(argv, budget, status_dir)
+        if rc == 0:
+            return 0
+        if known.no_fallback:
+            return rc
+        note = f"the single-process peer run failed ({why}); this line is the per-process run"
+        print(f"bench.py launcher: {note}; starting {known.gpus} fresh rank processes "
+              f"({deadline - time.monotonic():.0f} s left)", file=sys.stderr)
+    rank_argv = [*argv, "--procs", str(known.gpus)] if known.procs == 0 else argv
+    rc, failed = _run_ranks(rank_argv, known.gpus, deadline, known.launch_timeout, status_dir, note)
     if rc != 0 and failed and known.comm == "native" and not known.no_fallback:
         left = deadline - time.monotonic()
         if left > 30.0:
             print(f"bench.py launcher: retrying once with fresh rank processes and --comm torch "
                   f"({left:.0f} s left)", file=sys.stderr)
-            rc, _ = _run_ranks([*argv, "--comm", "torch"], known.gpus, deadline, known.launch_timeout, status_dir,
-                               "native RCCL communicator run failed; this line is the --comm torch rerun")
+            rerun = "native RCCL communicator run failed; this line is the --comm torch rerun"
+            rc, _ = _run_ranks([*rank_argv, "--comm", "torch"], known.gpus, deadline, known.launch_timeout,
+                               status_dir, f"{note}; {rerun}" if note else rerun)
     return rc
+
+
+def _run_one_process(argv: list[str], budget: float, status_dir: str) -> tuple[int, str]:
+    """Start ONE fresh ``bench.py --procs 1`` child for a ``--gpus N`` run and wait for it (at most
+    ``budget`` s; its own stage watchdog usually ends a hang first). Relays its single JSON line
+    when it exits 0; returns (exit code, why it failed). The parent touched no GPU: a failed child
+    is followed by fresh per-process ranks, never by re-executing anything that initialised one."""
+    import signal
+    import subprocess
+
+    env = dict(os.environ, BENCH_LAUNCHED_BY="bench.py (one process)", BENCH_STATUS_DIR=status_dir)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        (Path(status_dir) / "rank0").unlink()
+    except OSError:
+        pass
+    p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv, "--procs", "1"], env=env,
+                         stdout=subprocess.PIPE, stderr=None, text=True, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=budget)
+    except subprocess.TimeoutExpired:
+        stage = _stage_report(status_dir, 1, [0])
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.communicate()
+        return 1, f"still running after {budget:g} s; {stage.replace('rank 0', 'the process')}"
+    lines = [ln.strip() for ln in out.splitlines() if ln.lstrip().startswith("{")]
+    for ln in out.splitlines():
+        if not ln.lstrip().startswith("{"):
+            sys.stderr.write(ln + "\n")
+    if p.returncode == 0 and len(lines) == 1:
+        print(lines[0], flush=True)
+        return 0, ""
+    for ln in lines:  # a line that failed its result check: kept on stderr for the record
+        print(f"bench.py launcher: single-process line (not relayed): {ln}", file=sys.stderr)
+    if p.returncode == 0:
+        return 1, f"printed {len(lines)} JSON lines (expected 1)"
+    stage = _stage_report(status_dir, 1, []).replace("rank 0 exited, ", "")
+    return p.returncode or 1, f"exit status {p.returncode}, {stage}"
 
 
 def _run_ranks(argv: list[str], n: int, deadline: float, budget: float, status_dir: str,
@@ -249,7 +309,8 @@ class _Stages:
         self.rank, self.default, self.comm = rank, default_limit, comm
         d = os.environ.get("BENCH_STATUS_DIR")
         self.status = Path(d) / f"rank{rank}" if d else None
-        if default_limit > 0:
+        if default_limit > 0 and not getattr(self, "_watching", False):
+            self._watching = True  # one watchdog per process (a fallback path starts again)
             threading.Thread(target=self._watch, daemon=True).start()
 
     def enter(self, name: str, limit: float | None = None) -> None:
@@ -375,6 +436,102 @@ def make_clients(layout: ModelLayout, first_client: int, n: int, device: torch.d
         buckets[i].normal_(generator=g)
     views = [[buckets[i, o : o + m] for o, m in zip(offs, layout.numels)] for i in range(n)]
     return buckets, views
+
+
+def sample_elements(layout: ModelLayout, k_random: int = 4096, seed: int = 7) -> list[tuple[int, int]]:
+    """The (segment, index-in-segment) pairs a result check reads: every tensor's first and last
+    element plus ``k_random`` elements drawn uniformly over the model (seeded), in model order."""
+    rng = np.random.default_rng(seed)
+    starts = np.cumsum([0] + layout.numels[:-1])
+    picks = set()
+    for s, m in enumerate(layout.numels):
+        picks.update({(s, 0), (s, m - 1)})
+    for e in rng.integers(0, layout.total_numel, size=k_random):
+        s = int(np.searchsorted(starts, e, side="right") - 1)
+        picks.add((s, int(e - starts[s])))
+    return sorted(picks)
+
+
+def flat_index(layout: ModelLayout, picks: list[tuple[int, int]], elem_bytes: int, device: torch.device) -> torch.Tensor:
+    """Positions of ``picks`` in a padded flat buffer of the layout (ModelLayout.padded_offsets)."""
+    offs, _ = layout.padded_offsets(elem_bytes)
+    return torch.tensor([offs[s] + i for s, i in picks], dtype=torch.int64, device=device)
+
+
+def gather_client_samples(buckets: torch.Tensor, idx: torch.Tensor, first_client: int) -> tuple[np.ndarray, int]:
+    """The sampled elements of every resident client row ([n, K] fp64, exact) and how many rows
+    differ from their regeneration from the client's seed (make_clients): 0 = the inputs the
+    timed rounds read are intact — no stray store (a peer store that missed its slot) touched them."""
+    samples = buckets[:, idx].to(torch.float64).cpu().numpy()
+    g = torch.Generator(device=buckets.device)
+    scratch = torch.empty((1, buckets.shape[1]), dtype=buckets.dtype, device=buckets.device)
+    changed = 0
+    for i in range(buckets.shape[0]):
+        g.manual_seed(1234 + first_client + i)
+        scratch[0].normal_(generator=g)
+        changed += int(not torch.equal(scratch[0], buckets[i]))
+    del scratch
+    return samples, changed
+
+
+def _ordered_bits(a: np.ndarray) -> np.ndarray:
+    """IEEE bits mapped to a monotone integer line (+0 and -0 both at 0): ulp distance = difference."""
+    if a.dtype == np.float32:
+        i = a.view(np.int32).astype(np.int64)
+        return np.where(i < 0, -(i & 0x7FFFFFFF), i)
+    i = a.astype(np.float64).view(np.int64)
+    return np.where(i < 0, -(i & 0x7FFFFFFFFFFFFFFF), i)
+
+
+def result_check(got: np.ndarray, shards: list[np.ndarray], shard_weights: list[list[float]], out_dtype: str,
+                 exact: str | None) -> dict:
+    """Check sampled result elements against host fp64 compositions of the same clients
+    (fed_avg_algorithm.py:43-99: ``tmp = x.to(f64) * w; acc += tmp`` in arrival order, ``acc / W``).
+
+    ``shards[g]``: [n_g, K] fp64 client samples of entry / rank g in arrival order. ``exact``:
+    "single" — the one-GPU kernel, bit-identical to the reference's single chain; "composition" —
+    the peer exchange, bit-identical to each shard's chain summed in shard order; None — RCCL's
+    summation order, within the stated tolerance of the single chain (|Δ| ≤ 1e-12 · Σ|w x| / W in
+    fp64, ≤ 1 ulp after an fp32 cast — or |Δ| within that fp64 bound plus half an ulp of the output
+    where the result nearly cancels). Every form is also compared with the single chain."""
+    K = got.shape[0]
+    W = -0.0
+    for ws in shard_weights:
+        for w in ws:
+            W += w
+    parts, single, mag = [], np.full(K, -0.0), np.zeros(K)
+    for xs, ws in zip(shards, shard_weights):
+        acc = np.full(K, -0.0)
+        for x, w in zip(xs, ws):
+            acc = acc + x * w
+            single = single + x * w
+            mag = mag + np.abs(x * w)
+        if len(ws):
+            parts.append(acc)
+    comp = parts[0]
+    for p in parts[1:]:
+        comp = comp + p
+    npdt = np.float32 if out_dtype == "float32" else np.float64
+    want_single = (single / W).astype(npdt)
+    want_comp = (comp / W).astype(npdt)
+    got = got.astype(npdt)
+    bound = 1e-12 * mag / abs(W)
+    diff = np.abs(got.astype(np.float64) - single / W)
+    ulp = np.abs(_ordered_bits(got) - _ordered_bits(want_single))
+    if npdt == np.float64:
+        within = diff <= bound
+    else:
+        half_ulp = np.spacing(np.abs(want_single)).astype(np.float64) / 2
+        within = (ulp <= 1) | (diff <= bound + half_ulp)
+    bits_single = bool(np.array_equal(_ordered_bits(got), _ordered_bits(want_single)))
+    bits_comp = bool(np.array_equal(_ordered_bits(got), _ordered_bits(want_comp)))
+    ok = bool(np.all(within)) and (exact is None or (bits_single if exact == "single" else bits_comp))
+    return {
+        "elements": int(K), "expected": exact or "tolerance",
+        "bit_identical_to_single_chain": bits_single, "bit_identical_to_shard_composition": bits_comp,
+        "max_abs_vs_single_chain": float(np.abs(got.astype(np.float64) - want_single.astype(np.float64)).max()),
+        "max_ulp_vs_single_chain": int(ulp.max()), "within_tolerance": bool(np.all(within)), "ok": ok,
+    }
 
 
 def hbm_probes(device: torch.device, nbytes: int = 4 << 30) -> dict:
@@ -955,15 +1112,26 @@ def main_multi(args: argparse.Namespace) -> int:
     from distributed_learning_simulation_lib_amd.multi_device import MultiDeviceContext
 
     G = args.gpus
+    _STAGES.start(0, args.stage_timeout, "peer" if args.multi_exchange == "peer" else "native")
+    _STAGES.enter("create")
+    _inject_failure("one_process")
     devices = [0] * G if args.alias else list(range(G))
     if not args.alias and torch.cuda.device_count() < G:
-        raise SystemExit(f"--procs 1 --gpus {G}: only {torch.cuda.device_count()} GPU(s) visible (--alias rehearses)")
+        print(f"bench.py --procs 1 --gpus {G}: only {torch.cuda.device_count()} GPU(s) visible "
+              "(--alias rehearses)", file=sys.stderr)
+        return 3
     in_dtype, out_dtype = getattr(torch, args.in_dtype), getattr(torch, args.out_dtype)
     layout = LAYOUTS[args.layout]()
     P, T = layout.total_numel, layout.num_segments
     n_total = job_clients(args, G)
     weights_all = dataset_size_weights(n_total)
     m = MultiDeviceContext(layout, devices)
+    if args.multi_exchange == "peer" and not m.peer_access:
+        print(f"bench.py --procs 1: no peer access between the devices {devices}; the peer exchange "
+              "cannot run", file=sys.stderr)
+        m.close()
+        return 3
+    _STAGES.enter("make_clients")
     keep, tables = [], []
     for g, d in enumerate(devices):
         lo, hi = shard_bounds(n_total, G, g)
@@ -974,27 +1142,35 @@ def main_multi(args: argparse.Namespace) -> int:
         for row, w in zip(views, weights_all[lo:hi]):
             t.add_client(row, [w] * T)
         tables.append(t if hi > lo else None)
+    _STAGES.enter("plan")
     partials = m.plan_partials(tables, in_dtype)
     root_dev = torch.device("cuda", devices[0])
     offs, padded = layout.padded_offsets(out_dtype.itemsize)
     out_flat = torch.empty(padded, dtype=out_dtype, device=root_dev)
     outs = OutputTable([out_flat[o : o + n] for o, n in zip(offs, layout.numels)], layout, root_dev, out_dtype)
-    totals = [float(sum(weights_all))] * T
+    W = -0.0
+    for w in weights_all:
+        W += w
+    totals = [W] * T
     nt = m.num_tiles
     model = ExchangeModel()
     in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
     exchanges = (args.multi_exchange,)
     cands = exchange_candidates(args.chunks or None, exchanges=exchanges)
+    pending = [[(t, in_dtype)] if t is not None else [] for t in tables]
 
     def sync_all() -> None:
         for d in sorted(set(devices)):
             torch.cuda.synchronize(d)
 
     def one_round(ex: str, edges: list[int]) -> None:
+        # a round ends as the server's does, on the host: the NaN flags of every entry are read
+        # once the round's end event completed (one wait, like the one-GPU line's stream sync)
         m.round(partials, totals, outs, out_dtype, root=0, edges=edges, exchange=ex)
-        m.raise_on_nan([[(t, in_dtype)] if t is not None else [] for t in tables])
+        m.raise_on_nan(pending, round_only=True)
 
     tuned, selection = None, "cost model"
+    _STAGES.enter("tune", args.tune_budget + args.stage_timeout)
     if args.no_tune:
         (ex, ch, sh), _ = model.best(G, P, n_total, in_b, out_b, nt, cands, balance_root=False)
     else:
@@ -1014,9 +1190,11 @@ def main_multi(args: argparse.Namespace) -> int:
         tuned = {f"{a}/{b}/{c}": round(v, 4) for (a, b, c), v in times.items()}
         selection = "tuned"
     edges = chunk_edges(nt, ch, sh)
+    _STAGES.enter("warmup")
     for _ in range(args.warmup):
         one_round(ex, edges)
     sync_all()
+    _STAGES.enter("timed")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_round(ex, edges)
@@ -1026,8 +1204,25 @@ def main_multi(args: argparse.Namespace) -> int:
     job_bytes = n_total * P * in_b + P * out_b
     value = job_bytes / step_s / 1e9
 
+    # the result of the last timed round, sampled, against host fp64 compositions of the same
+    # clients (and every client row against its regeneration from its seed)
+    _STAGES.enter("result_check")
+    picks = sample_elements(layout)
+    got = out_flat[flat_index(layout, picks, out_b, root_dev)].to(torch.float64).cpu().numpy()
+    shards, shard_w, changed = [], [], 0
+    for g, d in enumerate(devices):
+        lo, hi = shard_bounds(n_total, G, g)
+        s, c = gather_client_samples(keep[g], flat_index(layout, picks, in_b, torch.device("cuda", d)), lo)
+        shards.append(s)
+        shard_w.append(weights_all[lo:hi])
+        changed += c
+    check = result_check(got, shards, shard_w, args.out_dtype, "composition" if ex == "peer" else None)
+    check["client_rows_changed"] = changed
+    check["ok"] = check["ok"] and changed == 0
+
     # the dominant kernel, after the timed region: entry 0's windowed partial launches (one per
     # chunk) timed with HIP events on its stream over the same number of rounds
+    _STAGES.enter("kernel_events")
     ctx0 = m.contexts[0]
     ctx0.prof_collect()
     ctx0.prof_enable(not args.no_kernel_events)
@@ -1042,7 +1237,9 @@ def main_multi(args: argparse.Namespace) -> int:
     achieved = rank_bytes / (kernel_step_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     predicted = model.round_ms(G, P, n_total, in_b, out_b, edges, ex) if G > 1 else None
     one_gpu = model.one_gpu_ms(P, n_total, in_b, out_b)
+    _STAGES.enter("teardown")
     m.close()
+    _STAGES.enter("done", 0)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": len(set(devices)), "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
@@ -1055,6 +1252,10 @@ def main_multi(args: argparse.Namespace) -> int:
             "parallelism": f"one process, {G} device entries: clients sharded, "
                            + ("peer-window exchange over xGMI (fedavg_multi_round)" if ex == "peer"
                               else "in-process RCCL reduce (fedavg_multi_round)"),
+            "launch": {"mode": "one process driving every GPU (bench.py --procs 1)",
+                       "launched_by": os.environ.get("BENCH_LAUNCHED_BY", "none"),
+                       "round_check": "per round: one event wait behind every entry's exchange, then the NaN "
+                                      "flags (fedavg_multi_round_check)"},
             "exchange": {"mode": ex, "chunks": ch, "chunk_shape": sh, "selection": selection,
                          "tuned_ms_per_round": tuned,
                          "predicted_speedup": None if predicted is None else predicted["speedup"],
@@ -1070,8 +1271,14 @@ def main_multi(args: argparse.Namespace) -> int:
             "bytes_per_step_this_rank": rank_bytes, "kernel_ms_per_step": round(kernel_step_ms, 4),
             "launches": launches,
         },
+        "result_check": check,
         "cpu_baseline": None,
     }
+    if not check["ok"]:
+        # not on stdout: a fallback run prints the job's one line
+        print(f"bench.py --procs 1: the result check failed; the line was: {json.dumps(line)}", file=sys.stderr,
+              flush=True)
+        return 3
     print(json.dumps(line), flush=True)
     return 0
 
@@ -1226,9 +1433,57 @@ def _rendezvous_env() -> None:
         os.environ["MASTER_PORT"] = str(_free_port())
 
 
+def _inject_failure(where: str) -> None:
+    """Test hook: BENCH_INJECT_FAIL=<where> makes that path exit with status 3 (the launcher's
+    fallback tests)."""
+    if os.environ.get("BENCH_INJECT_FAIL") == where:
+        print(f"bench.py: injected failure in the {where} run", file=sys.stderr, flush=True)
+        raise SystemExit(3)
+
+
+def main_dry_one_process(args: argparse.Namespace) -> int:
+    """--dry-run --procs 1 --gpus N: the single-process skeleton of main_multi on the CPU — stage
+    watchdog, client shards of the N device entries, the peer schedule of the cost model."""
+    G = args.gpus
+    _STAGES.start(0, args.stage_timeout, "peer")
+    _STAGES.enter("create")
+    _inject_failure("one_process")
+    layout = LAYOUTS[args.layout]()
+    n_total = job_clients(args, G)
+    shards = [list(shard_bounds(n_total, G, g)) for g in range(G)]
+    _STAGES.enter("timed")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    _ = time.perf_counter() - t0
+    model = ExchangeModel()
+    nt = -(-layout.total_numel // 4096)  # a 4096-element tile count of the order of the library's
+    (ex, ch, sh), pred = model.best(G, layout.total_numel, n_total, 4, 4, nt,
+                                    exchange_candidates(exchanges=("peer",)), balance_root=False)
+    _STAGES.enter("done", 0)
+    line = {
+        "metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": G, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+        "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "dry run: no client data, no GPU work",
+        "config": {"workload": workload_name(args, G, n_total, 1, n_total // G) + "_one_process",
+                   "total_clients": n_total, "params_per_client": layout.total_numel,
+                   "tensors_per_client": layout.num_segments, "client_shards": shards,
+                   "launch": {"mode": "one process", "devices": G},
+                   "exchange": {"mode": ex, "chunks": ch, "chunk_shape": sh, "selection": "cost model",
+                                "predicted_speedup": pred["speedup"]},
+                   "launched_by": os.environ.get("BENCH_LAUNCHED_BY", "none")},
+        "dry_run": "launcher check on the CPU: the single-process run's skeleton; not a measurement",
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main_dry(args: argparse.Namespace) -> int:
     """--dry-run: the multi-rank skeleton of main() on the CPU — gloo group, client shards, a
     barrier-bracketed timed region of empty steps, max over ranks, one JSON line from rank 0."""
+    if args.procs == 1 and args.gpus > 1:
+        return main_dry_one_process(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
@@ -1280,6 +1535,63 @@ def main_dry(args: argparse.Namespace) -> int:
         line["config"]["launch_fallback"] = os.environ["BENCH_LAUNCH_FALLBACK"]
     print(json.dumps(line), flush=True)
     return 0
+
+
+def _one_process_under_launcher(args: argparse.Namespace) -> bool:
+    """The default (``--procs 0``) under an external launcher (torch.distributed.run: WORLD_SIZE set,
+    every rank of one node): rank 0 drives every GPU in one process, as the self-launcher's child."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return (args.procs == 0 and world > 1 and world == args.gpus and args.workload == "fedavg"
+            and args.shard == "clients" and not args.rehearse
+            and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world)
+
+
+def main_one_process_under_launcher(args: argparse.Namespace) -> int | None:
+    """torch.distributed.run form of the default launch: rank 0 runs the single-process multi-device
+    round (main_multi: every GPU of the node, peer exchange) while the other ranks wait on a gloo
+    group; rank 0 broadcasts its exit status. 0: rank 0 printed the job's line and every rank exits
+    0. Otherwise (no peer access, a failed result check, an error) every rank returns None and the
+    same processes run the per-process path (fresh process group; rank 0 closed its multi-device
+    object; no process is re-executed), the line saying so in config.launch_fallback."""
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ.get("RANK", "0"))
+    _rendezvous_env()
+    budget = args.one_process_timeout + 60.0
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=budget))
+    status = torch.tensor([1], dtype=torch.int64)
+    if rank == 0:
+        os.environ.setdefault("BENCH_LAUNCHED_BY", "torch.distributed.run (rank 0 drives every GPU)")
+        one = argparse.Namespace(**vars(args))
+        one.procs = 1
+        try:
+            rc = main_dry_one_process(one) if args.dry_run else main_multi(one)
+        except SystemExit as e:
+            rc = e.code if isinstance(e.code, int) else 1
+        except Exception as e:  # noqa: BLE001 - any failure of the one-process run falls back
+            import traceback
+
+            traceback.print_exc()
+            print(f"bench.py rank 0: the one-process run raised {type(e).__name__}: {e}", file=sys.stderr)
+            rc = 1
+        status[0] = int(rc or 0)
+    dist.broadcast(status, src=0)
+    dist.destroy_process_group()
+    if int(status.item()) == 0:
+        return 0
+    note = (f"the single-process peer run on rank 0 failed (status {int(status.item())}); this line is the "
+            "per-process run of the same torch.distributed.run ranks")
+    os.environ["BENCH_LAUNCH_FALLBACK"] = note
+    os.environ.pop("BENCH_LAUNCHED_BY", None)
+    if rank == 0:
+        print(f"bench.py: {note}", file=sys.stderr, flush=True)
+        if not args.dry_run:
+            import gc
+
+            gc.collect()  # the one-process run's client buffers and receive slots, on every device
+            for d in range(torch.cuda.device_count()):
+                with torch.cuda.device(d):
+                    torch.cuda.empty_cache()
+    return None
 
 
 def main() -> int:
@@ -1348,8 +1660,12 @@ def main() -> int:
                     help="N > 1 with --exchange auto: seconds of exchange tuning before the best candidate "
                          "timed so far is taken")
     ap.add_argument("--procs", type=int, default=0,
-                    help="--procs 1 with --gpus N: one process drives the N GPUs (fedavg_multi_*, the "
-                         "single-process multi-device mode) instead of one rank process per GPU")
+                    help="--gpus N > 1: 1 = one process drives the N GPUs (fedavg_multi_*, the single-process "
+                         "multi-device mode, peer-window exchange); N = one rank process per GPU (RCCL); "
+                         "0 (default) = the one-process run, and fresh per-process ranks if it fails")
+    ap.add_argument("--one-process-timeout", type=float, default=200.0,
+                    help="--gpus N > 1 (default launch): seconds the one-process run may take before the "
+                         "launcher stops it and starts the per-process ranks (capped at half --launch-timeout)")
     ap.add_argument("--alias", action="store_true",
                     help="--procs 1: every device entry on cuda:0 (a one-GPU rehearsal of the multi-device round)")
     ap.add_argument("--multi-exchange", default="peer", choices=["peer", "reduce"],
@@ -1363,6 +1679,11 @@ def main() -> int:
         args.out_dtype = "float64" if args.workload in ("plugin", "gradient") else "float32"
     if args.clients_per_gpu is None:
         args.clients_per_gpu = 8 if args.workload == "gradient" else 64
+    if _one_process_under_launcher(args):
+        rc = main_one_process_under_launcher(args)
+        if rc is not None:
+            return rc
+        args.procs = args.gpus  # the one-process run failed: this rank continues per process
     if args.dry_run:
         return main_dry(args)
     if args.workload == "personalized":
@@ -1522,6 +1843,35 @@ def main() -> int:
 
     in_bytes = torch.empty((), dtype=in_dtype).element_size()
     out_bytes = torch.empty((), dtype=out_dtype).element_size()
+    # the result of the last timed round, sampled (every tensor's ends + 4096 random elements),
+    # against host fp64 compositions of the same clients; every client row is also compared with
+    # its regeneration from its seed. Rank 0 checks; the other ranks send their shards' samples.
+    if world > 1:
+        _STAGES.enter("result_check")
+    picks = sample_elements(layout)
+    s_local, changed = gather_client_samples(buckets, flat_index(layout, picks, in_bytes, device), lo)
+    bounds = [shard_bounds(n_total, world, r) for r in range(world)]
+    if dist.is_initialized():
+        xdev = torch.device("cpu") if args.rehearse else device
+        n_max = max(b - a for a, b in bounds)
+        mine = torch.zeros((n_max, len(picks)), dtype=torch.float64, device=xdev)
+        mine[:n_local] = torch.from_numpy(s_local).to(xdev)
+        every = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        ch = torch.tensor([changed], dtype=torch.int64, device=xdev)
+        dist.all_reduce(ch)
+        changed = int(ch.item())
+        shard_samples = [every[r][: b - a].cpu().numpy() for r, (a, b) in enumerate(bounds)]
+    else:
+        shard_samples = [s_local]
+    check = None
+    if rank == 0:
+        got = out_flat[flat_index(layout, picks, out_bytes, device)].to(torch.float64).cpu().numpy()
+        check = result_check(got, shard_samples, [weights_all[a:b] for a, b in bounds], args.out_dtype,
+                             "single" if world == 1 else None)
+        check["client_rows_changed"] = changed
+        check["ok"] = check["ok"] and changed == 0
+
     job_bytes = n_total * P * in_bytes + P * out_bytes
     step_s = elapsed / args.steps
     value_gbps = job_bytes / step_s / 1e9
@@ -1676,9 +2026,16 @@ def main() -> int:
         "input_only_GBps": round(n_total * P * in_bytes / step_s / 1e9, 2),
         "host_enqueue_ms_per_step": round(host_enqueue[0] * 1e3 / args.steps, 4),
         "hbm_probe": probe,
+        "result_check": check,
         "cpu_baseline": cpu,
     }
+    if world > 1:
+        line["config"]["launch"] = {"mode": f"one process per GPU ({world} ranks, torch.distributed)",
+                                    "launched_by": os.environ.get("BENCH_LAUNCHED_BY", "external launcher")}
     print(json.dumps(line), flush=True)
+    if check is not None and not check["ok"]:
+        print(f"bench.py: the result check failed: {json.dumps(check)}", file=sys.stderr, flush=True)
+        return 3
     return 0
 
 

@@ -159,6 +159,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
         c_int32, [c_void_p, _PP, _PD, _PP, c_int32, c_int32, POINTER(c_int32), c_int32, c_int32, _PP]),
     "fedavg_multi_combine": (c_int32, [c_void_p, _PD, _PP, c_int32, c_int32, c_int32, _PP]),
     "fedavg_multi_check": (c_int32, [c_void_p, POINTER(c_uint32)]),
+    "fedavg_multi_round_check": (c_int32, [c_void_p, POINTER(c_uint32)]),
     "fedavg_multi_reset": (c_int32, [c_void_p]),
 }
 

@@ -97,6 +97,7 @@ struct fedavg_multi {
   std::vector<std::vector<char>> tab_host;  // what each entry's table holds
   std::vector<hipEvent_t> start_ev;   // the caller's stream g, at round start
   std::vector<hipEvent_t> done_ev;    // entry j's last exchange work of the round
+  hipEvent_t end_ev = nullptr;        // entry 0's stream behind every entry's exchange work
   std::vector<std::vector<hipEvent_t>> part_ev;  // [g][chunk]
   // per entry g: its window table for the windowed partial launches — G slot pointers (device j's
   // receive slot for g) then [chunks][G + 1] tile edges — on device g, and its host image
@@ -256,6 +257,9 @@ int32_t order_round_end(fedavg_multi* m, void* const* streams) {
     hipStream_t s = stream_of(m, streams, g);
     for (int32_t j = 0; j < m->G; ++j) MULTI_HIP_TRY(hipStreamWaitEvent(s, m->done_ev[j], 0));
   }
+  // one event that completes after the whole round (fedavg_multi_round_check waits for it alone)
+  MULTI_HIP_TRY(hipSetDevice(m->devices[0]));
+  MULTI_HIP_TRY(hipEventRecord(m->end_ev, stream_of(m, streams, 0)));
   m->any_round = true;
   return FEDAVG_OK;
 }
@@ -359,6 +363,7 @@ int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t 
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&m->xstr[g], hipStreamNonBlocking, hi);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&m->start_ev[g], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&m->done_ev[g], hipEventDisableTiming);
+    if (e == hipSuccess && g == 0) e = hipEventCreateWithFlags(&m->end_ev, hipEventDisableTiming);
     if (e != hipSuccess)
       return bail(fedavg_internal_fail(FEDAVG_ERR_HIP, (std::string("multi-device streams: ") + hipGetErrorString(e)).c_str()));
     m->slots[g][g] = static_cast<double*>(fedavg_accumulator(m->ctx[g]));
@@ -413,6 +418,7 @@ int32_t fedavg_multi_destroy(fedavg_multi* m) {
     for (hipEvent_t ev : m->part_ev[j]) (void)hipEventDestroy(ev);
     if (m->start_ev[j]) (void)hipEventDestroy(m->start_ev[j]);
     if (m->done_ev[j]) (void)hipEventDestroy(m->done_ev[j]);
+    if (j == 0 && m->end_ev) (void)hipEventDestroy(m->end_ev);
     if (m->own[j]) (void)hipStreamDestroy(m->own[j]);
     if (m->xstr[j]) (void)hipStreamDestroy(m->xstr[j]);
     if (m->ctx[j]) (void)fedavg_ctx_destroy(m->ctx[j]);
@@ -641,6 +647,22 @@ int32_t fedavg_multi_check(fedavg_multi* m, uint32_t* flags_out) {
     MULTI_HIP_TRY(hipStreamSynchronize(m->xstr[g]));
     if (m->any_round) MULTI_HIP_TRY(hipEventSynchronize(m->done_ev[g]));
   }
+  for (int32_t g = 0; g < m->G; ++g) f |= fedavg_internal_flags(m->ctx[g], 0);
+  if (flags_out) *flags_out = f;
+  if (f & FEDAVG_FLAG_ACC_NAN) return fedavg_internal_fail(FEDAVG_ERR_NAN_ACCUM, "NaN in the accumulator");
+  if (f & FEDAVG_FLAG_RESULT_NAN) return fedavg_internal_fail(FEDAVG_ERR_NAN_RESULT, "NaN in the aggregated result");
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_multi_round_check(fedavg_multi* m, uint32_t* flags_out) {
+  DeviceRestore restore_device;
+  if (!m) return invalid("null multi-device object");
+  if (!m->any_round) return fedavg_multi_check(m, flags_out);
+  // the NaN words are host-coherent pinned memory the kernels store into at system scope: once
+  // the round's end event completed, every store of the round is visible here
+  MULTI_HIP_TRY(hipSetDevice(m->devices[0]));
+  MULTI_HIP_TRY(hipEventSynchronize(m->end_ev));
+  uint32_t f = 0;
   for (int32_t g = 0; g < m->G; ++g) f |= fedavg_internal_flags(m->ctx[g], 0);
   if (flags_out) *flags_out = f;
   if (f & FEDAVG_FLAG_ACC_NAN) return fedavg_internal_fail(FEDAVG_ERR_NAN_ACCUM, "NaN in the accumulator");

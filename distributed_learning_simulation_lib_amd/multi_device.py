@@ -138,10 +138,12 @@ class MultiDeviceContext:
         _native.check(self._lib.fedavg_multi_combine(self._h, tw, self._outs(outs, out_dtype, root), out_code(out_dtype),
                                                      root, exchange_code(exchange), self._streams()))
 
-    def flags(self) -> int:
-        """Synchronise every stream of the object; the OR of every entry's NaN flag bits."""
+    def flags(self, round_only: bool = False) -> int:
+        """Synchronise every stream of the object (``round_only``: wait for the end of the last
+        round / combine alone, ``fedavg_multi_round_check``); the OR of every entry's NaN flag bits."""
         f = ctypes.c_uint32()
-        st = self._lib.fedavg_multi_check(self._h, ctypes.byref(f))
+        fn = self._lib.fedavg_multi_round_check if round_only else self._lib.fedavg_multi_check
+        st = fn(self._h, ctypes.byref(f))
         if st not in (_native.OK, _native.ERR_NAN_ACCUM, _native.ERR_NAN_RESULT):
             _native.check(st)
         return int(f.value)
@@ -149,11 +151,13 @@ class MultiDeviceContext:
     def reset(self) -> None:
         _native.check(self._lib.fedavg_multi_reset(self._h))
 
-    def raise_on_nan(self, pending: Sequence[Sequence[tuple[ClientTable, torch.dtype]]] = ()) -> None:
+    def raise_on_nan(self, pending: Sequence[Sequence[tuple[ClientTable, torch.dtype]]] = (),
+                     round_only: bool = False) -> None:
         """The reference's assertions (fed_avg_algorithm.py:35,93,97) for the whole round: an input
         NaN in a table the caller still holds (``pending[g]``: entry g's tables) names its clients
-        (:35); otherwise a NaN sum (e.g. inf - inf across shards) is :93, a NaN quotient :97."""
-        f = self.flags()
+        (:35); otherwise a NaN sum (e.g. inf - inf across shards) is :93, a NaN quotient :97.
+        ``round_only``: the per-round form — wait for the last round's end event only."""
+        f = self.flags(round_only)
         if f == 0:
             return
         self.reset()

@@ -482,6 +482,10 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
  *       assertion). Resets every context's accumulated state (fed_avg_algorithm.py:90,98).
  *   fedavg_multi_check(m, flags_out): synchronise every stream of the object and report the OR
  *       of every context's NaN flags like fedavg_check; fedavg_multi_reset clears them.
+ *   fedavg_multi_round_check(m, flags_out): the same report after waiting for the end of the
+ *       last round / combine only (one event, behind every entry's exchange work) — the per-round
+ *       form of the reference's assertions (fed_avg_algorithm.py:35,93,97) for a server that
+ *       enqueued nothing else on the object's streams since; fedavg_multi_check before any round.
  * Results: each device's fold is the exact arrival-order chain of its clients; PEER sums the
  * partials in device order (bit-identical to that host composition), REDUCE in RCCL's order.
  * Every call returns with the caller's current device (hipGetDevice) unchanged. Destroy the
@@ -506,6 +510,7 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
 int32_t fedavg_multi_combine(fedavg_multi* m, const double* total_weights, void* const* out_ptrs, int32_t out_dtype,
                              int32_t root, int32_t exchange, void* const* streams);
 int32_t fedavg_multi_check(fedavg_multi* m, uint32_t* flags_out);
+int32_t fedavg_multi_round_check(fedavg_multi* m, uint32_t* flags_out);
 int32_t fedavg_multi_reset(fedavg_multi* m);
 
 #ifdef __cplusplus

@@ -32,10 +32,72 @@ def _json_lines(out: str) -> list[dict]:
 
 @pytest.mark.parametrize("world, shards", [
     (2, [[0, 128], [128, 256]]),
+    (4, [[0, 64], [64, 128], [128, 192], [192, 256]]),
+])
+def test_default_launch_is_one_process_driving_every_gpu(world, shards):
+    # the driver's exact command, `bench.py --gpus N`: ONE child process with --procs 1 (the
+    # single-process peer exchange), its line relayed
+    r = _run("--gpus", str(world), "--dry-run", "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["n_gpus"] == world
+    assert line["config"]["workload"] == f"fedavg_resnet18_fp32_256_clients_sharded_over_{world}_gpus_one_process"
+    assert line["config"]["client_shards"] == shards
+    assert line["config"]["launched_by"] == "bench.py (one process)"
+    assert line["config"]["launch"]["mode"] == "one process"
+    assert line["config"]["exchange"]["mode"] == "peer"
+    assert line["config"]["exchange"]["predicted_speedup"] > 1.0
+    assert "launch_fallback" not in line["config"]
+
+
+def test_failed_one_process_run_falls_back_to_fresh_rank_processes():
+    # an injected failure of the one-process run (as a missing peer access, a failed result
+    # check or its watchdog would end it): the launcher starts N fresh rank processes whose line
+    # says so
+    r = _run_env({"BENCH_INJECT_FAIL": "one_process"}, "--gpus", "2", "--dry-run", "--steps", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "injected failure in the one_process run" in r.stderr
+    assert "the single-process peer run failed (exit status 3" in r.stderr
+    (line,) = _json_lines(r.stdout)
+    assert line["config"]["launched_by"] == "bench.py"
+    assert line["config"]["client_shards"] == [[0, 128], [128, 256]]
+    assert "single-process peer run failed" in line["config"]["launch_fallback"]
+
+
+def test_hung_one_process_run_is_stopped_by_its_watchdog_then_falls_back():
+    import time as _time
+
+    t0 = _time.monotonic()
+    r = _run_env({"BENCH_INJECT_HANG": "0:timed:peer"}, "--gpus", "2", "--dry-run", "--steps", "2",
+                 "--stage-timeout", "4")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "rank 0: stage 'timed' still running after 4 s" in r.stderr
+    assert "exit status 124" in r.stderr and "last stage 'timed'" in r.stderr
+    (line,) = _json_lines(r.stdout)
+    assert line["config"]["launched_by"] == "bench.py"
+    assert _time.monotonic() - t0 < 120
+
+
+def test_one_process_budget_stops_a_run_without_watchdog():
+    r = _run_env({"BENCH_INJECT_HANG": "0:timed:peer"}, "--gpus", "2", "--dry-run", "--steps", "2",
+                 "--stage-timeout", "0", "--one-process-timeout", "6")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "still running after 6 s; the process still running, last stage 'timed'" in r.stderr
+    (line,) = _json_lines(r.stdout)
+    assert "single-process peer run failed" in line["config"]["launch_fallback"]
+
+
+def test_no_fallback_reports_the_one_process_failure():
+    r = _run_env({"BENCH_INJECT_FAIL": "one_process"}, "--gpus", "2", "--dry-run", "--no-fallback")
+    assert r.returncode != 0 and _json_lines(r.stdout) == []
+
+
+@pytest.mark.parametrize("world, shards", [
+    (2, [[0, 128], [128, 256]]),
     (3, [[0, 85], [85, 170], [170, 256]]),
 ])
 def test_launcher_spawns_ranks_and_relays_one_line(world, shards):
-    r = _run("--gpus", str(world), "--dry-run", "--steps", "3", "--warmup", "1")
+    r = _run("--gpus", str(world), "--procs", str(world), "--dry-run", "--steps", "3", "--warmup", "1")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
@@ -73,22 +135,48 @@ def test_launch_timeout_stops_the_ranks():
     assert "launch-timeout" in r.stderr
 
 
-def test_external_launcher_is_respected():
-    # the driver's torch.distributed.run form: WORLD_SIZE is set, bench.py spawns nothing
+def _torchrun(extra_env: dict, *args: str) -> subprocess.CompletedProcess:
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.setdefault("OMP_NUM_THREADS", "1")
+    env.update(extra_env)
     sys.path.insert(0, str(REPO))
     from bench import _free_port
 
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        str(REPO / "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2"],
-                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                           str(REPO / "bench.py"), "--gpus", "2", *args],
+                          cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+
+
+def test_external_launcher_is_respected():
+    # the driver's torch.distributed.run form with --procs 2: WORLD_SIZE is set, bench.py spawns
+    # nothing, every rank runs its shard
+    r = _torchrun({}, "--procs", "2", "--dry-run", "--steps", "2")
     assert r.returncode == 0, r.stderr[-3000:]
     (line,) = _json_lines(r.stdout)
     assert line["n_gpus"] == 2
     assert line["config"]["launched_by"] == "external launcher"
     assert line["config"]["workload"] == "fedavg_resnet18_fp32_256_clients_sharded_over_2_gpus"
+
+
+def test_external_launcher_default_is_rank_0_driving_every_gpu():
+    # the default under torch.distributed.run: rank 0 runs the one-process round over every GPU of
+    # the node while rank 1 waits; one line
+    r = _torchrun({}, "--dry-run", "--steps", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["n_gpus"] == 2
+    assert line["config"]["launched_by"] == "torch.distributed.run (rank 0 drives every GPU)"
+    assert line["config"]["exchange"]["mode"] == "peer"
+
+
+def test_external_launcher_falls_back_to_per_process_ranks_in_the_same_processes():
+    r = _torchrun({"BENCH_INJECT_FAIL": "one_process"}, "--dry-run", "--steps", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["config"]["launched_by"] == "external launcher"
+    assert line["config"]["workload"] == "fedavg_resnet18_fp32_256_clients_sharded_over_2_gpus"
+    assert "single-process peer run on rank 0 failed (status 3)" in line["config"]["launch_fallback"]
 
 
 def _run_env(extra_env: dict, *args: str, timeout: float = 240.0) -> subprocess.CompletedProcess:
@@ -107,7 +195,7 @@ def test_hung_native_rank_is_named_and_the_launcher_reruns_with_torch_comm():
     import time as _time
 
     t0 = _time.monotonic()
-    r = _run_env({"BENCH_INJECT_HANG": "1:timed:native"}, "--gpus", "2", "--dry-run", "--steps", "2",
+    r = _run_env({"BENCH_INJECT_HANG": "1:timed:native"}, "--gpus", "2", "--procs", "2", "--dry-run", "--steps", "2",
                  "--stage-timeout", "5")
     assert r.returncode == 0, r.stderr[-3000:]
     assert "rank 1: stage 'timed' still running after 5 s" in r.stderr
@@ -122,7 +210,7 @@ def test_a_hang_in_both_runs_fails_within_the_budget():
     import time as _time
 
     t0 = _time.monotonic()
-    r = _run_env({"BENCH_INJECT_HANG": "1:timed:any"}, "--gpus", "2", "--dry-run", "--stage-timeout", "4",
+    r = _run_env({"BENCH_INJECT_HANG": "1:timed:any"}, "--gpus", "2", "--procs", "2", "--dry-run", "--stage-timeout", "4",
                  "--launch-timeout", "100")
     assert r.returncode != 0 and _json_lines(r.stdout) == []
     # rank 1 hangs, rank 0 waits for it in the timed stage's collective: both watchdogs fire, in the
@@ -135,7 +223,7 @@ def test_a_hang_in_both_runs_fails_within_the_budget():
 def test_launch_timeout_names_the_stage_of_every_rank():
     # no watchdog (--stage-timeout 0): the launcher's own limit stops the run and says where each
     # rank was
-    r = _run_env({"BENCH_INJECT_HANG": "0:shards:any"}, "--gpus", "2", "--dry-run", "--stage-timeout", "0",
+    r = _run_env({"BENCH_INJECT_HANG": "0:shards:any"}, "--gpus", "2", "--procs", "2", "--dry-run", "--stage-timeout", "0",
                  "--launch-timeout", "20", "--no-fallback")
     assert r.returncode != 0
     assert "ranks still running after --launch-timeout 20 s" in r.stderr
@@ -147,17 +235,8 @@ def test_watchdog_fails_a_torchrun_job_fast():
     # the driver's launcher form: the hung rank ends itself, torchrun stops the job
     import time as _time
 
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env.setdefault("OMP_NUM_THREADS", "1")
-    env["BENCH_INJECT_HANG"] = "1:timed:any"
-    sys.path.insert(0, str(REPO))
-    from bench import _free_port
-
     t0 = _time.monotonic()
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        str(REPO / "bench.py"), "--gpus", "2", "--dry-run", "--stage-timeout", "5"],
-                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    r = _torchrun({"BENCH_INJECT_HANG": "1:timed:any"}, "--procs", "2", "--dry-run", "--stage-timeout", "5")
     assert r.returncode != 0
     # the hung rank or the one waiting for it in the stage's collective fires first; torchrun then
     # stops the other

@@ -24,17 +24,31 @@ from distributed_learning_simulation_lib_amd.build import LIB_DIR
 from distributed_learning_simulation_lib_amd.fedavg import ClientTable, ModelLayout, NaNAggregationError, OutputTable
 from distributed_learning_simulation_lib_amd.multi_device import MultiDeviceContext, window_bounds
 from distributed_learning_simulation_lib_amd.sharded import chunk_edges
-from oracle.fedavg_oracle import OracleFedAvg, OracleMessage, as_f64, complete, fedavg_flat, restore, sharded_composition
+from oracle.fedavg_oracle import OracleFedAvg, OracleMessage, as_f64, fedavg_flat, sharded_composition
 from tests.golden_hooks import make_hooked_class
 from tests.golden_io import bits_equal, load_golden
 from tests.test_gpu_parity import hook_spec
-from tests.test_oracle_golden import oracle_hooks
+from tests.multi_tolerance import reference_magnitude, sharded_expectation, ulp32, within_reference_tolerance
 
 pytestmark = pytest.mark.gpu
 CASES = load_golden()
 
 LAYOUT = ModelLayout(names=("conv", "bias", "fc", "one", "big", "odd"),
                      shapes=((16, 3, 3, 3), (16,), (10, 257), (1,), (3, 4096), (4096 * 2 + 13,)))
+
+
+def entry_devices(world: int, placement: str) -> list[int]:
+    """``aliased``: every entry on cuda:0 (the whole exchange on one GPU); ``distinct``: entries dealt
+    over every visible GPU (peer access, xGMI stores, cross-device events) — skipped on a one-GPU box."""
+    if placement == "aliased":
+        return [0] * world
+    count = torch.cuda.device_count()
+    if count < 2:
+        pytest.skip("distinct device entries need more than one GPU")
+    return [g % count for g in range(world)]
+
+
+PLACEMENTS = ["aliased", "distinct"]
 
 
 def _clients(n, dtype, seed):
@@ -47,20 +61,23 @@ def _owner(k, n, world, empty=None):
     return 0 if g == empty else g
 
 
+@pytest.mark.parametrize("placement", PLACEMENTS)
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.float64])
-def test_peer_round_is_the_sharded_composition(hip_device, world, dtype):
+def test_peer_round_is_the_sharded_composition(hip_device, world, dtype, placement):
     n = 11
     rng = np.random.default_rng(world)
     weights = [int(w) for w in rng.integers(1, 5000, n)] if dtype != torch.float64 else \
         [float(w) for w in rng.uniform(0.1, 9.0, n)]
     clients = _clients(n, dtype, 3 + world)
-    m = MultiDeviceContext(LAYOUT, [0] * world)
+    devices = entry_devices(world, placement)
+    m = MultiDeviceContext(LAYOUT, devices)
     try:
         assert m.peer_access and m.world == world
         tables = [ClientTable(LAYOUT.num_segments) for _ in range(world)]
         for k, c in enumerate(clients):
-            tables[_owner(k, n, world)].add_client([t.to(hip_device) for t in c], [weights[k]] * LAYOUT.num_segments)
+            g = _owner(k, n, world)
+            tables[g].add_client([t.to(torch.device("cuda", devices[g])) for t in c], [weights[k]] * LAYOUT.num_segments)
         partials = m.plan_partials(tables, dtype)
         W = -0.0
         for w in weights:
@@ -84,9 +101,17 @@ def test_peer_round_is_the_sharded_composition(hip_device, world, dtype):
                             assert bits_equal(got, want), (edges, root, s)
                         else:
                             assert np.array_equal(got.view(np.uint32), want.astype(np.float32).view(np.uint32)), s
+                        # against the reference's single chain: fp64 within 1e-12 of sum |w x| / W,
+                        # the fp32 casts at most 1 ulp apart (the device result itself, both dtypes)
                         single = fedavg_flat([clients[k][s].numpy() for k in range(n)], weights)
                         mag = sum(np.abs(as_f64(clients[k][s].numpy())) * abs(weights[k]) for k in range(n)) / W
                         assert np.all(np.abs(want - single) <= 1e-12 * mag)
+                        if out_dtype == torch.float64:
+                            ok, why = within_reference_tolerance(got, single, mag)
+                        else:  # an fp32 result: the 1-ulp form of the bound
+                            u = ulp32(got, single)
+                            ok, why = bool(u.size == 0 or u.max() <= 1), f"{u.max()} ulp"
+                        assert ok, (edges, root, s, why)
     finally:
         m.close()
 
@@ -189,45 +214,9 @@ def test_window_bounds_partition_every_chunk():
 
 
 # ---- the plugin surface: FedAVGAlgorithm(devices=[...]) ---------------------------------------------
-def sharded_expectation(case, world):
-    """The host composition of a golden case dealt round-robin over ``world`` entries (the plugin's
-    assignment): per entry the oracle's sums, summed in entry order, divided by the arrival-order
-    totals through the case's _apply_total_weight hook. Per-element weights stay on entry 0 (one
-    chain: the reference's own result)."""
-    get_weight, apply_total = oracle_hooks(case)
-    if case.weight_mode is not None and case.weight_mode.startswith("elementwise"):
-        return case.expected
-    full = OracleFedAvg(get_weight=get_weight, apply_total_weight=apply_total)
-    lanes = [OracleFedAvg(get_weight=get_weight) for _ in range(world)]
-    kinds = case.kinds or ["full"] * len(case.arrivals)
-    i = 0
-    for a, kind in zip(case.arrivals, kinds):
-        if a.arrays is None:
-            continue
-        params = dict(a.arrays)
-        if kind == "delta":
-            params = restore(params, case.old)
-        elif case.old is not None:
-            complete(params, case.old)
-        full.process_worker_data(a.worker_id, OracleMessage(parameter=dict(params), aggregation_weight=a.weight,
-                                                            dtype=case.dtype))
-        lanes[i % world].process_worker_data(a.worker_id, OracleMessage(parameter=dict(params),
-                                                                        aggregation_weight=a.weight, dtype=case.dtype))
-        i += 1
-    out = {}
-    for name in full._acc:
-        parts = [ln._acc[name] for ln in lanes if name in ln._acc]
-        s = parts[0]
-        for p in parts[1:]:
-            s = s + p
-        assert not np.isnan(s).any()
-        out[name] = full._apply_total_weight(name, s, full._totals[name])
-        assert not np.isnan(out[name]).any()
-    return out
-
-
-def run_multi(case, device, world, wave_size, from_host=False):
-    algo = make_hooked_class(FedAVGAlgorithm, hook_spec(case))(devices=[device] * world, wave_size=wave_size)
+def run_multi(case, device, world, wave_size, from_host=False, devices=None):
+    algo = make_hooked_class(FedAVGAlgorithm, hook_spec(case))(devices=devices or [device] * world,
+                                                                 wave_size=wave_size)
     algo.accumulate = case.accumulate
     algo.aggregate_loss = case.aggregate_loss
     kinds = case.kinds or ["full"] * len(case.arrivals)
@@ -267,12 +256,32 @@ def test_plugin_devices_golden_cases(name, world, wave_size, hip_device):
     res = run_multi(case, hip_device, world, wave_size, from_host=(wave_size == 3))
     assert list(res.parameter.keys()) == case.meta["out_keys"]
     want = case.expected if not case.accumulate else sharded_expectation(case, world)
+    mag = reference_magnitude(case) if case.accumulate else None
     for k, v in want.items():
         got = res.parameter[k]
         assert got.dtype == torch.float64 and tuple(got.shape) == v.shape and got.device == hip_device
         assert bits_equal(got.cpu().numpy(), v), f"{name}/{k}"
+        if mag is not None:  # and against the reference's single chain at the stated tolerance
+            ok, why = within_reference_tolerance(got.cpu().numpy(), case.expected[k], mag[k])
+            assert ok, f"{name}/{k}: {why}"
     assert res.other_data == case.meta["result_other_data"]
     assert res.in_round == case.meta["in_round"] and res.end_training == case.meta["end_training"]
+
+
+@pytest.mark.parametrize("name", sorted(n for n, c in CASES.items() if c.error is None and c.accumulate))
+def test_plugin_distinct_devices_golden_cases(name, hip_device):
+    """The plugin over every visible GPU (skipped on a one-GPU box): peer loads of the entries'
+    accumulators across devices, the result on the first entry's GPU."""
+    case = CASES[name]
+    devices = [torch.device("cuda", d) for d in entry_devices(torch.cuda.device_count(), "distinct")]
+    res = run_multi(case, devices[0], len(devices), 3, devices=devices)
+    want = sharded_expectation(case, len(devices))
+    mag = reference_magnitude(case)
+    for k, v in want.items():
+        got = res.parameter[k]
+        assert got.device == devices[0] and bits_equal(got.cpu().numpy(), v), f"{name}/{k}"
+        ok, why = within_reference_tolerance(got.cpu().numpy(), case.expected[k], mag[k])
+        assert ok, f"{name}/{k}: {why}"
 
 
 @pytest.mark.parametrize("world", [2, 4])

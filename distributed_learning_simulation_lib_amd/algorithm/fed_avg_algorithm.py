@@ -106,6 +106,17 @@ def _total_is_fp32(weight: Any) -> bool:
 
 
 class FedAVGAlgorithm(AggregationAlgorithm):
+    """The reference's ``FedAVGAlgorithm`` (fed_avg_algorithm.py:12-149) folding on MI355X.
+
+    One device (``device``, the default): every result is bit-identical to the reference's single
+    arrival-order fp64 chain. ``devices=[...]`` (one server process, several GPUs): arrivals are
+    dealt to the entries in turn and each entry's chain is summed in entry order, so a result
+    depends on the entry count and on which client lands on which entry, and matches the
+    reference's single chain to fp64 reassociation only — |Δ| ≤ 1e-12 · Σ|w x| / |W| per element,
+    ≤ 1 ulp after an fp32 cast (tests/test_multi_tolerance.py, tests/test_gpu_multi_device.py);
+    ``bit_exact_with_reference`` says which of the two a given object gives.
+    """
+
     def __init__(
         self,
         device: torch.device | str | None = None,
@@ -187,6 +198,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__lane = 0
         self.__arrivals = 0
         self.exchange = exchange
+        self.bit_exact_with_reference = True
         if devices is not None:
             devs = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in devices]
             if not devs or any(d.type != "cuda" for d in devs):
@@ -195,6 +207,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 raise ValueError("device must be the first entry of devices (the result's device)")
             self._device = devs[0]
             self.__multi_devices = devs
+            # entry-ordered sums of per-entry chains: the reference's result to fp64 reassociation
+            self.bit_exact_with_reference = len(devs) == 1
             self.__lanes = [{a: getattr(self, a) for a in _LANE_ATTRS} for _ in devs]
             for lane, d in zip(self.__lanes, devs):
                 lane["_device"] = d

@@ -62,7 +62,8 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         # dtype codes of this round's natively staged arrivals (None once one took the general path)
         self.__native_codes: set[int] | None = set()
         self.__ptr_rows: list[bytes] = []  # the natively staged arrivals' device addresses
-        self.__weights_memo: tuple | None = None  # (receivers, arrival ids, [M][N] weights)
+        # ((receivers, arrival ids), [M][N] weights, copies of the receivers' weight dicts)
+        self.__weights_memo: tuple | None = None
         self.__geometry: tuple | None = None  # (native layout, offsets, flat size, shapes)
         # (key, [(buffer, views)] per receiver, (buffer, views) centralized) of the last round's
         # result buffers, written again only while nobody outside can see them (_result_rows)
@@ -268,18 +269,22 @@ class PersonalizedFedAVGAlgorithm(AggregationAlgorithm):
         return memo[1], memo[2], memo[3]
 
     def _weights(self, receivers: list[int], ids: list[int]) -> np.ndarray:
-        """weights[r][n] = worker_weights[receiver r].get(arrival n's worker, 0) (:36); the
-        matrix of the last (receivers, arrival order) is kept (the weights are set once)."""
+        """weights[r][n] = worker_weights[receiver r].get(arrival n's worker, 0) (:36). The
+        reference reads the caller's dicts live on every arrival, so the matrix of the last
+        (receivers, arrival order) is reused only while every receiver's dict still equals the copy
+        taken with it (one C-level dict comparison per receiver): a caller that changes a weight in
+        place between rounds gets it, as in the reference."""
         key = (tuple(receivers), tuple(ids))
         memo = self.__weights_memo
-        if memo is not None and memo[0] == key:
+        if (memo is not None and memo[0] == key
+                and all(self._worker_weights[j] == snap for j, snap in zip(receivers, memo[2]))):
             return memo[1]
         weights = np.zeros((len(receivers), len(ids)), dtype=np.float64)
         for r, j in enumerate(receivers):
             wj = self._worker_weights[j]
             for n, wid in enumerate(ids):
                 weights[r, n] = float(wj.get(wid, 0))
-        self.__weights_memo = (key, weights)
+        self.__weights_memo = (key, weights, [dict(self._worker_weights[j]) for j in receivers])
         return weights
 
     @staticmethod

@@ -88,10 +88,17 @@ struct fedavg_multi {
   std::vector<hipStream_t> xstr;  // the high-priority exchange stream of each entry
   bool peer_ok = true;
   std::string peer_error;
-  // slots[j][g]: entry j's receive buffer for entry g's partial (accumulator coordinates);
-  // slots[j][j] is entry j's own accumulator
+  // slots[j][g]: entry j's receive buffer for entry g's partial of entry j's windows, the windows of
+  // a round's chunks packed one after the other (slot_cap[j] elements: 1/G of the accumulator,
+  // not all of it); slots[j][j] is entry j's own accumulator. A launch addresses a window through
+  // a pointer rebased by the window's accumulator offset (rebased()), so the kernels keep
+  // accumulator coordinates.
   std::vector<std::vector<double*>> slots;
   std::vector<std::vector<bool>> slot_owned;
+  std::vector<int64_t> slot_cap;
+  // this round's windows: [j][chunk] accumulator start of window j of the chunk and its offset in
+  // the packed slot (both multiples of FEDAVG_ACC_ALIGN elements)
+  std::vector<std::vector<int64_t>> win_acc, win_off;
   // per entry: the combine's device table, T fp64 totals then T output pointers
   std::vector<char*> tab_dev;
   std::vector<std::vector<char>> tab_host;  // what each entry's table holds
@@ -99,13 +106,14 @@ struct fedavg_multi {
   std::vector<hipEvent_t> done_ev;    // entry j's last exchange work of the round
   hipEvent_t end_ev = nullptr;        // entry 0's stream behind every entry's exchange work
   std::vector<std::vector<hipEvent_t>> part_ev;  // [g][chunk]
-  // per entry g: its window table for the windowed partial launches — G slot pointers (device j's
-  // receive slot for g) then [chunks][G + 1] tile edges — on device g, and its host image
+  // per entry g: its window table for the windowed partial launches — [chunks][G] rebased slot
+  // pointers (device j's receive slot for g) then [chunks][G + 1] tile edges — on device g, and its
+  // host image
   std::vector<char*> win_dev;
   std::vector<size_t> win_cap;
   std::vector<std::vector<char>> win_host;
-  // per entry j: the own-window combine's source table — slots[j][h] for the round's members h —
-  // on device j, and its host image
+  // per entry j: the own-window combine's source tables — [chunks][FEDAVG_MULTI_MAX_DEVICES]
+  // rebased slots[j][h] for the round's members h — on device j, and its host image
   std::vector<char*> comb_dev;
   std::vector<std::vector<char>> comb_host;
   bool any_round = false;
@@ -130,18 +138,62 @@ int32_t ensure_part_events(fedavg_multi* m, int32_t chunks) {
   return FEDAVG_OK;
 }
 
-int32_t ensure_slots(fedavg_multi* m) {
-  for (int32_t j = 0; j < m->G; ++j) {
+int64_t align_up(int64_t n) { return (n + FEDAVG_ACC_ALIGN - 1) / FEDAVG_ACC_ALIGN * FEDAVG_ACC_ALIGN; }
+
+// The windows of this round's chunks and receive slots big enough for them. Window j of chunk k
+// covers tiles [e_k + span*j/G, e_k + span*(j+1)/G) = accumulator elements [a, b); entry j's slots
+// pack its windows in chunk order, each rounded up to the accumulator alignment. A slot is
+// reallocated (after every device drained: a peer may still write the old one) only when a new
+// chunking needs more than it holds.
+int32_t ensure_slots(fedavg_multi* m, const std::vector<int32_t>& edges) {
+  const int32_t G = m->G, chunks = static_cast<int32_t>(edges.size()) - 1;
+  m->win_acc.assign(G, std::vector<int64_t>(chunks, 0));
+  m->win_off.assign(G, std::vector<int64_t>(chunks, 0));
+  std::vector<int64_t> need(G, 0);
+  for (int32_t k = 0; k < chunks; ++k) {
+    const int64_t tb = edges[k], span = edges[k + 1] - edges[k];
+    for (int32_t j = 0; j < G; ++j) {
+      const int32_t wb = static_cast<int32_t>(tb + span * j / G), we = static_cast<int32_t>(tb + span * (j + 1) / G);
+      int64_t a = 0, b = 0;
+      if (wb < we)
+        if (int32_t st = fedavg_tile_range(m->ctx[j], wb, we, &a, &b)) return st;
+      m->win_acc[j][k] = a;
+      m->win_off[j][k] = need[j];
+      need[j] += align_up(b - a);
+    }
+  }
+  bool grow = false;
+  for (int32_t j = 0; j < G; ++j) grow = grow || need[j] > m->slot_cap[j];
+  if (!grow) return FEDAVG_OK;
+  for (int32_t g = 0; g < G; ++g) {
+    MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
+    MULTI_HIP_TRY(hipDeviceSynchronize());
+  }
+  for (int32_t j = 0; j < G; ++j) {
+    if (need[j] <= m->slot_cap[j]) continue;
     MULTI_HIP_TRY(hipSetDevice(m->devices[j]));
-    for (int32_t g = 0; g < m->G; ++g) {
-      if (m->slots[j][g]) continue;
+    for (int32_t g = 0; g < G; ++g) {
+      if (g == j) continue;
+      if (m->slot_owned[j][g] && m->slots[j][g]) MULTI_HIP_TRY(hipFree(m->slots[j][g]));
+      m->slots[j][g] = nullptr;
       double* p = nullptr;
-      MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p), sizeof(double) * static_cast<size_t>(m->acc_numel)));
+      MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p), sizeof(double) * static_cast<size_t>(need[j])));
       m->slots[j][g] = p;
       m->slot_owned[j][g] = true;
     }
+    m->slot_cap[j] = need[j];
   }
   return FEDAVG_OK;
+}
+
+// Where entry g's partial of window (j, chunk k) goes, in accumulator coordinates: entry j's slot
+// for g rebased by the window's accumulator start (a kernel adds the tile's accumulator offset);
+// entry j's own partial stays in its accumulator.
+double* rebased(const fedavg_multi* m, int32_t j, int32_t g, int32_t k) {
+  if (g == j) return m->slots[j][j];
+  const uintptr_t base = reinterpret_cast<uintptr_t>(m->slots[j][g]);
+  return reinterpret_cast<double*>(base + sizeof(double) * static_cast<uintptr_t>(m->win_off[j][k]) -
+                                   sizeof(double) * static_cast<uintptr_t>(m->win_acc[j][k]));
 }
 
 // Entry j's combine table (totals, outputs); re-uploaded only when it changes (once per plan in a
@@ -161,16 +213,18 @@ int32_t upload_tables(fedavg_multi* m, const double* totals, void* const* outs) 
   return FEDAVG_OK;
 }
 
-// Entry g's window table for this round's chunk edges (re-uploaded only when the edges change, after
-// the device finished the launches that read the old one).
+// Entry g's window table for this round's chunk edges (re-uploaded only when the edges or the slots
+// change, after the device finished the launches that read the old one).
 int32_t upload_windows(fedavg_multi* m, const std::vector<int32_t>& edges) {
   const int32_t G = m->G, chunks = static_cast<int32_t>(edges.size()) - 1;
+  const size_t ptr_bytes = sizeof(double*) * static_cast<size_t>(chunks) * G;
   for (int32_t g = 0; g < G; ++g) {
-    std::vector<char> img(sizeof(double*) * G + sizeof(int32_t) * static_cast<size_t>(chunks) * (G + 1));
-    for (int32_t j = 0; j < G; ++j) std::memcpy(img.data() + sizeof(double*) * j, &m->slots[j][g], sizeof(double*));
-    auto* e = reinterpret_cast<int32_t*>(img.data() + sizeof(double*) * G);
+    std::vector<char> img(ptr_bytes + sizeof(int32_t) * static_cast<size_t>(chunks) * (G + 1));
+    auto* dst = reinterpret_cast<double**>(img.data());
+    auto* e = reinterpret_cast<int32_t*>(img.data() + ptr_bytes);
     for (int32_t k = 0; k < chunks; ++k) {
       const int64_t tb = edges[k], span = edges[k + 1] - edges[k];
+      for (int32_t j = 0; j < G; ++j) dst[k * G + j] = rebased(m, j, g, k);
       for (int32_t j = 0; j <= G; ++j) e[k * (G + 1) + j] = static_cast<int32_t>(tb + span * j / G);
     }
     if (m->win_host[g] == img) continue;
@@ -189,18 +243,28 @@ int32_t upload_windows(fedavg_multi* m, const std::vector<int32_t>& edges) {
   return FEDAVG_OK;
 }
 
-// Entry j's own-window combine sources for this round's members (re-uploaded when they change,
-// after entry j's exchange stream stopped reading the old table).
-int32_t upload_comb(fedavg_multi* m, const std::vector<int32_t>& members) {
+// Entry j's own-window combine sources for this round's members and chunks (re-uploaded when they
+// change, after entry j's exchange stream stopped reading the old table).
+int32_t upload_comb(fedavg_multi* m, const std::vector<int32_t>& members, int32_t chunks) {
+  const size_t need = sizeof(double*) * FEDAVG_MULTI_MAX_DEVICES * static_cast<size_t>(chunks);
   for (int32_t j = 0; j < m->G; ++j) {
-    std::vector<char> img(sizeof(double*) * FEDAVG_MULTI_MAX_DEVICES, 0);
-    for (size_t i = 0; i < members.size(); ++i) std::memcpy(img.data() + sizeof(double*) * i, &m->slots[j][members[i]], sizeof(double*));
-    if (m->comb_host[j] == img) continue;
+    // the image keeps the allocation's size (a round of fewer chunks leaves the tail as it was)
+    std::vector<char> img(std::max(need, m->comb_host[j].size()), 0);
+    auto* src = reinterpret_cast<double**>(img.data());
+    for (int32_t k = 0; k < chunks; ++k)
+      for (size_t i = 0; i < members.size(); ++i) src[k * FEDAVG_MULTI_MAX_DEVICES + i] = rebased(m, j, members[i], k);
+    if (m->comb_host[j].size() == img.size() &&
+        std::memcmp(m->comb_host[j].data(), img.data(), need) == 0)
+      continue;
     MULTI_HIP_TRY(hipSetDevice(m->devices[j]));
     MULTI_HIP_TRY(hipStreamSynchronize(m->xstr[j]));
-    if (!m->comb_dev[j]) MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->comb_dev[j]), img.size()));
-    MULTI_HIP_TRY(hipMemcpy(m->comb_dev[j], img.data(), img.size(), hipMemcpyHostToDevice));
-    m->comb_host[j] = img;
+    if (m->comb_host[j].size() < img.size()) {
+      if (m->comb_dev[j]) MULTI_HIP_TRY(hipFree(m->comb_dev[j]));
+      m->comb_dev[j] = nullptr;
+      MULTI_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&m->comb_dev[j]), img.size()));
+    }
+    MULTI_HIP_TRY(hipMemcpy(m->comb_dev[j], img.data(), need, hipMemcpyHostToDevice));
+    m->comb_host[j] = img;  // only its first `need` bytes are compared
   }
   return FEDAVG_OK;
 }
@@ -338,6 +402,7 @@ int32_t fedavg_multi_create(fedavg_multi** out, const int32_t* devices, int32_t 
   m->xstr.assign(m->G, nullptr);
   m->slots.assign(m->G, std::vector<double*>(m->G, nullptr));
   m->slot_owned.assign(m->G, std::vector<bool>(m->G, false));
+  m->slot_cap.assign(m->G, 0);
   m->tab_dev.assign(m->G, nullptr);
   m->tab_host.assign(m->G, {});
   m->start_ev.assign(m->G, nullptr);
@@ -468,11 +533,11 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
   if (exchange == FEDAVG_EXCHANGE_PEER) {
     if (!m->peer_ok) return invalid(("the peer exchange needs peer access: " + m->peer_error).c_str());
     if (static_cast<int32_t>(members.size()) > FEDAVG_MULTI_MAX_DEVICES) return invalid("too many devices");
-    if (int32_t st = ensure_slots(m)) return st;
+    if (int32_t st = ensure_slots(m, edges)) return st;
     if (int32_t st = ensure_part_events(m, chunks)) return st;
     if (int32_t st = upload_tables(m, total_weights, out_ptrs)) return st;
     if (int32_t st = upload_windows(m, edges)) return st;
-    if (int32_t st = upload_comb(m, members)) return st;
+    if (int32_t st = upload_comb(m, members, chunks)) return st;
     if (int32_t st = order_round_start(m, streams)) return st;
     const int32_t vec = outs_aligned(out_ptrs, m->T, out_dtype) ? 1 : 0;
     // a member with a dense plan folds its own window last, with the other members' partials of
@@ -501,8 +566,10 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
           for (const auto& r : ranges) {
             if (r[0] >= r[1]) continue;
             if (int32_t st = fedavg_internal_plan_run_windows(
-                    partials[g], r[0], r[1], s, reinterpret_cast<double* const*>(wt),
-                    reinterpret_cast<const int32_t*>(wt + sizeof(double*) * m->G) + k * (m->G + 1), m->G))
+                    partials[g], r[0], r[1], s, reinterpret_cast<double* const*>(wt) + static_cast<size_t>(k) * m->G,
+                    reinterpret_cast<const int32_t*>(wt + sizeof(double*) * static_cast<size_t>(chunks) * m->G) +
+                        k * (m->G + 1),
+                    m->G))
               return st;
           }
         } else {
@@ -511,7 +578,7 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
             int32_t wb = 0, we = 0;
             window(j, wb, we);
             if (wb == we) continue;
-            if (int32_t st = fedavg_internal_plan_run_range_to(partials[g], wb, we, s, m->slots[j][g])) return st;
+            if (int32_t st = fedavg_internal_plan_run_range_to(partials[g], wb, we, s, rebased(m, j, g, k))) return st;
           }
         }
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
@@ -526,14 +593,15 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
           for (int32_t g : members)
             if (g != j) MULTI_HIP_TRY(hipStreamWaitEvent(m->xstr[j], m->part_ev[g][k], 0));
           if (int32_t st = fedavg_internal_plan_run_comb(
-                  partials[j], wb, we, m->xstr[j], reinterpret_cast<const double* const*>(m->comb_dev[j]),
+                  partials[j], wb, we, m->xstr[j],
+                  reinterpret_cast<const double* const*>(m->comb_dev[j]) + static_cast<size_t>(k) * FEDAVG_MULTI_MAX_DEVICES,
                   static_cast<int32_t>(members.size()), rank_of[j], total_weights, out_ptrs, out_dtype))
             return st;
           continue;
         }
         for (int32_t g : members) MULTI_HIP_TRY(hipStreamWaitEvent(m->xstr[j], m->part_ev[g][k], 0));
         std::vector<const double*> src;
-        for (int32_t g : members) src.push_back(m->slots[j][g]);
+        for (int32_t g : members) src.push_back(rebased(m, j, g, k));
         const char* tab = m->tab_dev[j];
         if (int32_t st = fedavg_internal_multi_combine(
                 m->ctx[j], wb, we, src.data(), static_cast<int32_t>(src.size()), reinterpret_cast<const double*>(tab),

@@ -80,6 +80,9 @@ static_assert(kJB == 8 || kJB == 16, "receivers per wave");
 #define PERS_U 2
 #endif
 constexpr int kU = PERS_U;             // clients loaded ahead per lane
+#ifndef PERS_PTR_AHEAD  // register pipeline: client pointers loaded one group ahead
+#define PERS_PTR_AHEAD 1
+#endif
 // Whole aligned fp32 / fp64 chunks of the fused (FMA) fold stream clients through an LDS-DMA ring;
 // the separately rounded fold keeps the register pipeline (VALU-bound: the ring measured 3 % slower
 // there). Weight rows staged through the ring, and a one-client-ahead weight prefetch, measured
@@ -574,13 +577,26 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
     const int n = a.Npad;
     kp<double> wk = wt;  // weight row of client k + u, advanced incrementally
     const int64_t wstep = a.wstride;
+#if PERS_PTR_AHEAD
+    // the next group's client pointers are loaded one group ahead, with the first client's high
+    // weights (a scalar load waited at once per group otherwise exposed its whole latency)
+    uint64_t pn[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pn[u] = ptrs[(kU + u < n) ? kU + u : u];
+#endif
     for (int k = 0; k < n; k += kU) {
       RT cur[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) cur[u] = nxt[u];
       const int kn = (k + kU < n) ? k + kU : k;  // the last group re-loads itself (L2 hits)
+#if PERS_PTR_AHEAD
+#pragma unroll
+      for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(pn[u], sb, zeros), e, count);
+      const int kn2 = (kn + kU < n) ? kn + kU : kn;
+#else
 #pragma unroll
       for (int u = 0; u < kU; ++u) nxt[u] = load_raw<T, FULL>(client_base(ptrs[kn + u], sb, zeros), e, count);
+#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
@@ -590,6 +606,12 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
         double whi[H];
 #pragma unroll
         for (int j = 0; j < H; ++j) whi[j] = wk[H + j];
+#if PERS_PTR_AHEAD
+        if (u == 0) {
+#pragma unroll
+          for (int q = 0; q < kU; ++q) pn[q] = ptrs[kn2 + q];
+        }
+#endif
         __builtin_amdgcn_sched_barrier(0);
         double x[kVE];
         R::expand(cur[u], x);
@@ -602,7 +624,7 @@ __device__ __forceinline__ void pers_body(const PArgs& a, int wave, int lane, in
 #pragma unroll
         for (int j = 0; j < H; ++j) wlo[j] = w1[j];
         __builtin_amdgcn_sched_barrier(0);
-        fold_half<FOLD, H, H, false, !std::is_same<T, double>::value>(acc, x, whi);
+        fold_half<FOLD, H, H, PERS_PTR_AHEAD != 0, !std::is_same<T, double>::value>(acc, x, whi);
         __builtin_amdgcn_sched_barrier(0);
         wk = w1;
       }

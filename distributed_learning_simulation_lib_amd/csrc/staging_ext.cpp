@@ -14,6 +14,8 @@
 #include <torch/extension.h>
 
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace {
@@ -232,6 +234,30 @@ py::object row_pointers(py::list row, py::list numels, int64_t device_index, int
 // attributes, no autograd state, no names) and each still has the geometry views() gave it.
 // Anything else — a result the caller kept, a view of a result, its storage object, an in-place
 // reshape — answers false and the caller allocates a fresh buffer, as every round did before.
+//
+// Sharing a storage with another process leaves every count above unchanged: torch.multiprocessing
+// swaps the storage's DataPtr for one whose deleter parks the block in its IPC limbo (CUDA tensors:
+// CudaIPCSentData) or moves it to shared memory (host tensors), so the buffer must also still carry
+// the deleter of the allocator that made it — the one a fresh allocation with its options gets.
+bool allocator_owned(const at::Tensor& flat) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, c10::DeleterFnPtr> native;  // (device type, index) -> deleter
+  const std::pair<int, int> key{static_cast<int>(flat.device().type()), static_cast<int>(flat.device().index())};
+  c10::DeleterFnPtr want = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = native.find(key);
+    if (it != native.end()) want = it->second;
+  }
+  if (want == nullptr) {
+    const at::Tensor probe = at::empty({1}, flat.options());
+    want = probe.storage().data_ptr().get_deleter();
+    std::lock_guard<std::mutex> lock(mu);
+    native[key] = want;
+  }
+  return want != nullptr && flat.storage().data_ptr().get_deleter() == want;
+}
+
 bool unobserved(const at::Tensor& flat, py::list views, py::list offsets, py::list shapes) {
   const Py_ssize_t T = PyList_GET_SIZE(views.ptr());
   const ShapeSet* shp = g_shapes.get(shapes.ptr());
@@ -240,6 +266,7 @@ bool unobserved(const at::Tensor& flat, py::list views, py::list offsets, py::li
     return false;
   const c10::Storage& st = flat.storage();
   if (st.use_count() != 1 + static_cast<int64_t>(T)) return false;
+  if (!allocator_owned(flat)) return false;
   const char* base = static_cast<const char*>(st.data()) + flat.storage_offset() * flat.itemsize();
   for (Py_ssize_t t = 0; t < T; ++t) {
     PyObject* o = PyList_GET_ITEM(views.ptr(), t);

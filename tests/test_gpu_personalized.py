@@ -123,6 +123,25 @@ def _assert_same(res, want, result_dtype=torch.float64):
 SHAPES = {"conv": (32, 16, 3, 3), "bn": (32,), "fc": (10, 300), "odd": (1001,), "s": ()}
 
 
+def test_weights_changed_in_place_between_rounds_are_used(hip_device):
+    """The reference reads ``worker_weights[j][i]`` live on every arrival (:34): a caller that edits
+    a receiver's dict in place between rounds (no new set_worker_weights) gets the new weights."""
+    n = 6
+    clients, ww = _random_round(n, range(n), SHAPES, 17)
+    live = {j: dict(v) for j, v in ww.items()}
+    algo = PersonalizedFedAVGAlgorithm(device=hip_device)
+    algo.set_worker_weights(live)
+    for rnd in range(3):
+        for k, p in enumerate(clients):
+            algo.process_worker_data(k, ParameterMessage(parameter={m: t.to(hip_device) for m, t in p.items()}))
+        res = algo.aggregate_worker_data()
+        algo.clear_worker_data()
+        _assert_same(res, _oracle(clients, live))
+        live[2][4] = 0.25 * (rnd + 2)  # in place, seen by the next round
+        live[3].pop(1, None)
+    algo.exit()
+
+
 @pytest.mark.parametrize("weight_kind", ["float", "int"])
 def test_random_round_matches_oracle(hip_device, weight_kind):
     clients, ww = _random_round(24, range(24), SHAPES, 101, weight_kind=weight_kind)
@@ -224,4 +243,19 @@ def test_result_buffers_reused_only_when_unobserved(hip_device):
     assert res3.worker_data[5].parameter["conv"].data_ptr() != conv5.data_ptr()
     assert bits_equal(conv5.cpu().numpy(), want2.worker_data[5].parameter["conv"])
     _assert_same(kept, kept_want)
+    # receiver 3's model sent to its worker process (PipeServerEndpoint.broadcast of a
+    # MultipleWorkerMessage through torch.multiprocessing, aggregation_server.py:202): never written
+    # again once the server let go of it
+    import gc
+    from multiprocessing.reduction import ForkingPickler
+
+    import torch.multiprocessing as _torch_mp  # noqa: F401  (registers the tensor reducers)
+
+    sent = res3.worker_data[3].parameter["fc"].data_ptr()
+    payload = ForkingPickler.dumps(res3.worker_data[3].parameter)
+    del res3
+    gc.collect()
+    res4, _ = one_round(4)
+    assert res4.worker_data[3].parameter["fc"].data_ptr() != sent
+    del payload
     algo.exit()

@@ -233,4 +233,19 @@ def test_result_buffer_reuse_never_changes_a_kept_result(hip_device, devices):
     assert again["fc"].data_ptr() == ptr
     for n, v in kept_want.items():
         assert bits_equal(kept[n].cpu().numpy(), v), n
+    # a result sent to another process (what PipeServerEndpoint.broadcast of the result does with
+    # torch.multiprocessing: CUDA IPC, the counts unchanged) is never written again, even after the
+    # server dropped every reference to it
+    import gc
+    from multiprocessing.reduction import ForkingPickler
+
+    import torch.multiprocessing as _torch_mp  # noqa: F401  (registers the tensor reducers)
+
+    sent_ptr = again["fc"].data_ptr()
+    payload = ForkingPickler.dumps(again["fc"])
+    del again
+    gc.collect()
+    fresh, _ = one_round(30)
+    assert fresh["fc"].data_ptr() != sent_ptr
+    del payload
     algo.exit()

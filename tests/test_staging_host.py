@@ -130,6 +130,26 @@ def test_result_buffer_is_reused_only_when_nobody_can_see_it():
     assert not ext.unobserved(flat, views, offs, shapes)
 
 
+def test_a_buffer_shared_with_another_process_is_never_reused():
+    """torch.multiprocessing sharing leaves the reference counts as they were but moves the buffer
+    (host: into shared memory; CUDA: behind the IPC limbo's deleter): ``unobserved`` also requires
+    the allocator's own deleter, so such a buffer is never written again."""
+    from multiprocessing.reduction import ForkingPickler
+
+    import torch.multiprocessing as _torch_mp  # noqa: F401  (registers the tensor reducers)
+
+    flat = torch.zeros(40, dtype=torch.float64)
+    offs, shapes = [0, 8, 24], [(2, 4), (4, 4), (3,)]
+    views = ext.views(flat, offs, shapes)
+    assert ext.unobserved(flat, views, offs, shapes)
+    payload = ForkingPickler.dumps(views[1])  # what a Queue / Pipe put of the result does
+    import gc
+
+    gc.collect()
+    assert not ext.unobserved(flat, views, offs, shapes)
+    del payload
+
+
 def test_table_arguments_reach_a_c_abi_pointer_parameter():
     """fedavg._table_args: the native table's raw addresses and a ClientTable's numpy arrays both
     pass through a c_void_p parameter (the hot entry points' client table arguments) with the

@@ -572,8 +572,15 @@ def host_cpu() -> dict:
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         usable = None
-    return {"model": model, "usable_cpus": usable, "machine_cpus": os.cpu_count(),
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    out = {"model": model, "usable_cpus": usable, "machine_cpus": os.cpu_count(),
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and usable and int(omp) < usable:
+        # the GPU pool runs one GPU's job per box share: OMP_NUM_THREADS is set to that share
+        # (16 CPUs per GPU) by the harness, while the affinity mask shows the whole machine
+        out["cores_note"] = (f"timed on OMP_NUM_THREADS={omp} threads: the harness's per-GPU CPU share on this "
+                             f"box (its affinity mask shows all {usable} CPUs of the machine, shared by 8 GPUs' jobs)")
+    return out
 
 
 def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dtype: torch.dtype = torch.float32) -> dict:

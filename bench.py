@@ -1550,21 +1550,26 @@ def _one_process_under_launcher(args: argparse.Namespace) -> bool:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     return (args.procs == 0 and world > 1 and world == args.gpus and args.workload == "fedavg"
             and args.shard == "clients" and not args.rehearse
-            and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world)
+            and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+            # the ranks meet on torch.distributed.run's own store (no process group is created here,
+            # so the per-process fallback can still create its own)
+            and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True")
 
 
 def main_one_process_under_launcher(args: argparse.Namespace) -> int | None:
     """torch.distributed.run form of the default launch: rank 0 runs the single-process multi-device
-    round (main_multi: every GPU of the node, peer exchange) while the other ranks wait on a gloo
-    group; rank 0 broadcasts its exit status. 0: rank 0 printed the job's line and every rank exits
+    round (main_multi: every GPU of the node, peer exchange) while the other ranks wait on
+    torch.distributed.run's own store for its exit status (no process group: the fallback below
+    creates the job's one). 0: rank 0 printed the job's line and every rank exits
     0. Otherwise (no peer access, a failed result check, an error) every rank returns None and the
     same processes run the per-process path (fresh process group; rank 0 closed its multi-device
     object; no process is re-executed), the line saying so in config.launch_fallback."""
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ.get("RANK", "0"))
-    _rendezvous_env()
     budget = args.one_process_timeout + 60.0
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=budget))
+    store = dist.PrefixStore("bench_one_process", dist.TCPStore(
+        os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, is_master=False,
+        timeout=timedelta(seconds=budget)))
     status = torch.tensor([1], dtype=torch.int64)
     if rank == 0:
         os.environ.setdefault("BENCH_LAUNCHED_BY", "torch.distributed.run (rank 0 drives every GPU)")
@@ -1581,8 +1586,10 @@ def main_one_process_under_launcher(args: argparse.Namespace) -> int | None:
             print(f"bench.py rank 0: the one-process run raised {type(e).__name__}: {e}", file=sys.stderr)
             rc = 1
         status[0] = int(rc or 0)
-    dist.broadcast(status, src=0)
-    dist.destroy_process_group()
+        store.set("status", str(int(status.item())))
+    else:
+        store.wait(["status"])
+        status[0] = int(store.get("status").decode())
     if int(status.item()) == 0:
         return 0
     note = (f"the single-process peer run on rank 0 failed (status {int(status.item())}); this line is the "

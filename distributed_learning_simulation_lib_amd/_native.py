@@ -147,6 +147,11 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_sharded_round_edges": (
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int32), c_int32, c_int32, c_int32, c_void_p]),
+    # dynamic waves (dyn_wave_kernel)
+    "fedavg_dyn_open": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
+    "fedavg_dyn_publish": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, POINTER(c_int32)]),
+    "fedavg_dyn_close": (c_int32, [c_void_p, _PP, c_int32, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    "fedavg_dyn_state": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     # single-process multi-device mode (multi_device.cpp)
     "fedavg_multi_create": (c_int32, [POINTER(c_void_p), POINTER(c_int32), c_int32, POINTER(c_int64), c_int32, _PP]),
     "fedavg_multi_destroy": (c_int32, [c_void_p]),

@@ -115,3 +115,34 @@ class NativeClientTable:
 
     def elementwise_arrays(self):
         raise NotImplementedError("per-element weights need fedavg.ClientTable")
+
+
+class TableTail:
+    """Rows [offset, n) of a NativeClientTable (the ClientTable protocol): what the ordinary
+    waves still fold after a dynamic wave folded rows [0, offset) (fedavg_dyn_close)."""
+
+    def __init__(self, table: NativeClientTable, offset: int) -> None:
+        self.table = table
+        self.offset = int(offset)
+        self.num_segments = table.num_segments
+        self.device_index = table.device_index
+
+    @property
+    def num_clients(self) -> int:
+        return self.table.num_clients - self.offset
+
+    def validate(self, numels, esize: int, device_index: int, key) -> None:
+        self.table.validate(numels, esize, device_index, key)
+
+    def arrays(self):
+        p, w = self.table.arrays()
+        o = self.offset * self.num_segments
+        return p[o:], w[o:]
+
+    def addresses(self) -> tuple[int, int]:
+        p, w = self.table.addresses()
+        o = self.offset * self.num_segments * 8
+        return p + o, w + o
+
+    def elementwise_arrays(self):
+        raise NotImplementedError("per-element weights need fedavg.ClientTable")

@@ -43,7 +43,7 @@ import numpy as np
 import torch
 
 from .. import _native, _staging
-from .._staging import NativeClientTable
+from .._staging import NativeClientTable, TableTail
 from ..fedavg import ClientTable, FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
 from ..ingest import HostIngest
 from ..multi_device import MultiDeviceContext
@@ -70,6 +70,7 @@ from .aggregation_algorithm import (
 _KERNEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
 _STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # staging_ext.cpp codes
 _STAGING_CODES = {dt: code for code, dt in enumerate(_STAGING_DTYPES)}
+_DYN_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # dyn_wave_kernel inputs
 # host QSGD records packed by pointer (FEDAVG_QSGD_HOST_PTRS=0: through per-record views, A/B knob)
 _HOST_RECORD_PTRS = os.environ.get("FEDAVG_QSGD_HOST_PTRS", "1") != "0"
 # what a device entry of the multi-device mode keeps for itself (the rest of the round's state —
@@ -128,6 +129,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         devices: Sequence[int | str | torch.device] | None = None,
         exchange: str = "peer",
         wave_min: int | None = None,
+        dynamic_wave: bool | None = None,
     ) -> None:
         super().__init__()
         self.accumulate: bool = True
@@ -145,6 +147,19 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.wave_min = int(os.environ.get("FEDAVG_WAVE_MIN", 0) if wave_min is None else wave_min)
         assert self.wave_min >= 0
         self.__wave_event: torch.cuda.Event | None = None  # recorded after each flushed wave
+        # The round's first wave as a dynamic wave (include/fedavg_hip.h fedavg_dyn_*): launched at
+        # the round's first staged update, handed the staged rows every FEDAVG_DYN_BATCH arrivals
+        # while it folds the ones it has, closed by the wave's flush or by aggregate_worker_data
+        # (which then divides in the same kernel) — the GPU works through the arrival phase instead
+        # of after it. Any update it cannot take (an absent tensor, per-tensor weights, unaligned
+        # tensors) or a current stream with unfinished work closes it early: it keeps the rows it
+        # folded and the ordinary waves fold the rest, with the same bits.
+        self.dynamic_wave = (os.environ.get("FEDAVG_DYN", "1") != "0") if dynamic_wave is None else bool(dynamic_wave)
+        self.__dyn_batch = max(1, int(os.environ.get("FEDAVG_DYN_BATCH", 4)))
+        self.__dyn_table: Any = None         # the table the open dynamic wave reads
+        self.__dyn_pub = 0                   # its rows published so far
+        self.__dyn_closed: Any = None        # (table, rows folded) of the round's closed dynamic wave
+        self.__dyn_round = False             # the round's first wave has been decided
         self.result_dtype = result_dtype
         self.result_device = torch.device(result_device) if result_device is not None else None
         self.split_policy = split_policy
@@ -483,6 +498,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self._all_worker_data[worker_id] = worker_data
         self.__has_data = True
         worker_data.parameter = {}
+        self._dyn_arrival()
         return True
 
     def _stage_natively(self, params: Any, w: Any, delta: bool = False) -> bool:
@@ -539,6 +555,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     self.__table_delta = delta
                 self.__ew = False
                 self.__has_data = True
+                self._dyn_arrival()
                 return True
         first = next(iter(params.values()), None)
         host = isinstance(first, torch.Tensor) and first.device.type == "cpu"
@@ -791,6 +808,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         else:
             self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
         self.__has_data = True
+        if type(self.__table) is NativeClientTable:
+            self._dyn_arrival()
 
     def _scan_arrival(self, tensors: list, dt: Any, worker_id: int | None, delta: bool) -> None:
         """fed_avg_algorithm.py:34-35 at the arrival: one GPU scan of the staged update."""
@@ -897,6 +916,57 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         ev = self.__wave_event
         return ev is None or ev.query()
 
+    # ---- the dynamic wave (fedavg_dyn_*) ------------------------------------------------
+    def _dyn_arrival(self) -> None:
+        """A row joined the wave's native table: open the round's dynamic wave at the first one
+        (when the round qualifies), then hand it the staged rows every ``FEDAVG_DYN_BATCH``."""
+        table = self.__table
+        if self.__dyn_table is None:
+            if self.__dyn_round:
+                return
+            self.__dyn_round = True
+            if not (self.dynamic_wave and type(table) is NativeClientTable and table.num_clients == 1
+                    and self.device.type == "cuda"
+                    and self.__multi_devices is None and self.accumulate and self.__default_hooks
+                    and not self.wave_min and not self.eager_nan_check and self.__ew is False
+                    and not self.__table_delta and self.__table_dtype in _DYN_DTYPES):
+                return
+            try:
+                self._context().dyn_open(self.__table_dtype, self.wave_size)
+            except _native.NativeError:
+                return  # e.g. the accumulator already holds data: the ordinary waves
+            self.__dyn_table, self.__dyn_pub, self.__dyn_closed = table, 0, None
+        elif self.__dyn_table is not table:
+            return
+        if table.num_clients - self.__dyn_pub >= self.__dyn_batch:
+            self._dyn_publish()
+
+    def _dyn_publish(self) -> None:
+        """Every staged row of the dynamic wave's table to the wave (none while the current stream
+        has unfinished work); a row it cannot take closes it with the rows it has."""
+        try:
+            self.__dyn_pub += self._context().dyn_publish(self.__dyn_table)
+        except _native.NativeError:
+            self._dyn_close(None)
+
+    def _dyn_close(self, outs: Any, out_dtype: torch.dtype = torch.float64) -> bool:
+        """Close the open dynamic wave: into ``outs`` (True: the round's result is written) or into
+        the accumulator (the rows it folded; ``_dyn_rest`` gives the ordinary calls the rest)."""
+        table = self.__dyn_table
+        self.__dyn_table = None
+        folded, finalized = self._context().dyn_close(outs, out_dtype)
+        self.__dyn_closed = (table, folded)
+        return finalized
+
+    def _dyn_rest(self, table: Any) -> Any:
+        """The part of ``table`` the ordinary calls fold: all of it, its rows after those a closed
+        dynamic wave folded (``TableTail``), or None when the wave folded every row."""
+        closed = self.__dyn_closed
+        if closed is None or closed[0] is not table or not closed[1]:
+            return table
+        self.__dyn_closed = None
+        return TableTail(table, closed[1]) if closed[1] < table.num_clients else None
+
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""
         if self.__table is None or self.__table.num_clients == 0:
@@ -905,6 +975,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         table, dt = self.__table, self.__table_dtype
         assert dt is not None
         self.__table, self.__table_dtype = None, None
+        if self.__dyn_table is table:  # a full dynamic wave: its rows stay in the accumulator
+            self._dyn_publish()
+            self._dyn_close(None)
+        table = self._dyn_rest(table)
+        if table is None:
+            return
         if self.__ew:
             ctx.accumulate_elementwise(table, dt, self._ew_totals_buffer(), self._tot_fp32_flags())
         elif self.__table_delta:
@@ -949,6 +1025,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return out
 
     def _reset_round(self) -> None:
+        if self.__dyn_table is not None:  # an abandoned round's dynamic wave ends with its rows
+            try:
+                self._dyn_close(None)
+            except _native.NativeError:
+                pass
+        self.__dyn_closed, self.__dyn_round = None, False
         self.__arrivals = 0
         self.__has_data = False
         self.__host_totals = {}
@@ -1002,8 +1084,16 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         flat, outs, views = self._result_buffer(out_dtype, reuse=not custom_divide)
         self.__result_flat = None if custom_divide else flat
         delta = self.__table_delta and table is not None
+        done = False  # the dynamic wave wrote the result
+        if table is not None and self.__dyn_table is table:
+            self._dyn_publish()
+            done = self._dyn_close(None if (self.__ew or custom_divide or host_divide or delta) else outs, out_dtype)
+        if not done and table is not None:
+            table = self._dyn_rest(table)
         try:
-            if self.__ew:
+            if done:
+                pass
+            elif self.__ew:
                 if table is not None and dt is not None:
                     ctx.accumulate_elementwise(table, dt, self._ew_totals_buffer(), self._tot_fp32_flags())
                 if not custom_divide:

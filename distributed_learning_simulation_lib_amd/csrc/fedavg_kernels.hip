@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -842,6 +843,317 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS)) void fedavg_tile_k
       }
     }
     if constexpr (SPLIT > 1) break;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Dynamic wave: the round's first wave folded while its clients are still arriving.
+//
+// The plugin round (FedAVGAlgorithm.process_worker_data x N, then aggregate_worker_data:
+// fed_avg_algorithm.py:20-113, driven by aggregation_server.py:111-145) stages every arrival on
+// the host; a wave launched only once all N are staged leaves the GPU idle for the whole
+// arrival phase. This kernel is launched at the round's first arrival with an open client count:
+// the host publishes staged rows into a host-coherent table (fedavg_dyn_publish) and the kernel
+// folds them as they appear, in arrival order, into fp64 accumulators held in registers; the
+// round's close (fedavg_dyn_close) fixes the count and either divides into the outputs (the
+// fused `_apply_total_weight`, :71-97) or stores the accumulator (a partial wave the ordinary
+// waves continue from). Per element the fold is the reference's chain — acc = -0.0, then
+// acc + round(x * w) per client in arrival order — so the bits are those of the one-launch
+// kernel.
+//
+// Workgroup 0 is the mirror: one thread polls the host control words over PCIe and republishes
+// the row count in device memory, so the tile workgroups poll device memory only; it also ends
+// the wave by itself (state 2, accumulator mode) when the host publishes nothing for `idle`
+// ticks or the wave outlives `life` ticks, and acknowledges every close in host memory — the
+// host learns from that acknowledgement how many rows were folded. Every workgroup leaves once
+// the mirror closed (tile workgroups also after `life` + a margin on their own): no wave spins
+// past the wave's lifetime. All stores are vector stores (global_store with scope bits).
+struct DynCtl {     // host-coherent, written by the host
+  uint32_t count;   // rows published (release)
+  uint32_t closed;  // 1: `count` is final
+  uint32_t mode;    // at close: OUT_ACC / OUT_F32 / OUT_F64
+  uint32_t pad;
+};
+struct DynAck {     // host-coherent, written by the mirror workgroup
+  uint32_t state;   // 0 running, 1 closed by the host, 2 closed by the kernel (idle / lifetime)
+  uint32_t count;   // rows the wave folds
+  uint32_t error;   // 1: a tile workgroup gave up waiting for the mirror
+  uint32_t pad;
+};
+struct DynMirror {  // device memory, written by the mirror workgroup: one copy per XCD (kDynCopies,
+  uint32_t count;   // a cache line apart), so the tile workgroups' polls spread over 8 lines
+  uint32_t closed;
+  uint32_t mode;
+  uint32_t pad[13];
+};
+constexpr int kDynCopies = 8;
+struct DynArgs {
+  const TileDesc* tiles;
+  const SegDesc* segs;
+  double* acc;
+  uint32_t* flag;
+  DynCtl* ctl;              // device aliases of the host-coherent block
+  DynAck* ack;
+  const uint64_t* ptab;     // [T][cap] client pointers, segment-major
+  const double* wtab;       // [cap] client weights
+  const double* wtot;       // [T] divisors (final close)
+  const uint64_t* outs;     // [T] output pointers (final close)
+  DynMirror* mir;
+  int32_t num_tiles;
+  int32_t cap;
+  uint64_t idle_ticks;      // s_memrealtime ticks (100 MHz)
+  uint64_t life_ticks;
+};
+
+constexpr int kDynBatch = 64;  // rows a tile workgroup fetches per poll (one per lane of wave 0)
+
+__device__ __forceinline__ uint32_t dyn_ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t dyn_ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void dyn_mirror(const DynArgs& a) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t last = t0;
+  uint32_t mc = 0;
+  for (;;) {
+    const uint32_t hc = dyn_ld_sys(&a.ctl->count);
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (dyn_ld_sys(&a.ctl->closed)) {
+      const uint32_t fc = dyn_ld_sys(&a.ctl->count);
+      const uint32_t mode = dyn_ld_sys(&a.ctl->mode);
+      for (int i = 0; i < kDynCopies; ++i) {
+        __hip_atomic_store(&a.mir[i].mode, mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.mir[i].count, fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.mir[i].closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(&a.ack->count, fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.ack->state, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    if (hc > mc) {
+      mc = hc;
+      last = now;
+      for (int i = 0; i < kDynCopies; ++i)
+        __hip_atomic_store(&a.mir[i].count, mc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (now - last > a.idle_ticks || now - t0 > a.life_ticks) {
+      // nothing new for too long (or too long alive): the wave ends with the rows seen so far
+      for (int i = 0; i < kDynCopies; ++i) {
+        __hip_atomic_store(&a.mir[i].mode, static_cast<uint32_t>(OUT_ACC), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.mir[i].count, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.mir[i].closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(&a.ack->count, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.ack->state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__((Geo<T, 1, kTile1>::THREADS)) void dyn_wave_kernel(DynArgs a) {
+  if (blockIdx.x == 0) {
+    dyn_mirror(a);
+    return;
+  }
+  constexpr int AE = Geo<T, 1, kTile1>::AE;
+  constexpr int LANES = Geo<T, 1, kTile1>::LANES;
+  constexpr int TILE = Geo<T, 1, kTile1>::TILE;
+  using LL = LaneLoader<T, LANES, true, true, AE>;
+  using LC = LaneLoader<T, LANES, false, true, AE>;
+  using V = typename LL::V;
+  constexpr int N = LL::N;
+  constexpr int VPL = LL::VPL;
+  constexpr int CU_LOADS = (FEDAVG_CU_BYTES / (VPL * 16)) < 2 ? 2 : (FEDAVG_CU_BYTES / (VPL * 16));
+  __shared__ uint64_t sp[kDynBatch];
+  __shared__ double sw[kDynBatch];
+  __shared__ int32_t s_n;
+  __shared__ int32_t s_mode;
+  __shared__ double s_W;
+  __shared__ uint64_t s_out;
+
+  const TileDesc td = load_tile(a.tiles, blockIdx.x - 1);
+  const int seg = td.seg;
+  const int count = td.count;
+  const bool full = count == TILE;
+  const int li = static_cast<int>(threadIdx.x);
+  const int64_t elem_off = td.start * static_cast<int64_t>(sizeof(T));
+  const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;  // SegDesc::acc_off
+
+  double acc[AE];
+#pragma unroll
+  for (int i = 0; i < AE; ++i) acc[i] = -0.0;  // the additive identity (see tile_body)
+
+  DynMirror* const mir = a.mir + (blockIdx.x % kDynCopies);
+  int k = 0;             // rows folded
+  uint32_t avail = 0;    // rows known published (thread 0)
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t closed = 0;
+      while (avail <= static_cast<uint32_t>(k) && !closed) {
+        const uint32_t c = dyn_ld_agent(&mir->count);
+        if (c > avail) {
+          avail = c;
+          break;
+        }
+        if (dyn_ld_agent(&mir->closed)) {
+          avail = dyn_ld_agent(&mir->count);
+          closed = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.life_ticks + 100000000ull) {  // life + 1 s
+          __hip_atomic_store(&a.ack->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          avail = static_cast<uint32_t>(k);
+          closed = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(16);
+      }
+      const int n = static_cast<int>(avail) - k;
+      s_n = n < 0 ? 0 : (n > kDynBatch ? kDynBatch : n);
+    }
+    __syncthreads();
+    const int n = __builtin_amdgcn_readfirstlane(s_n);
+    if (n == 0) break;
+    if (li < n) {  // the batch's rows of this tile's segment, straight from the host table
+      sp[li] = __hip_atomic_load(a.ptab + static_cast<int64_t>(seg) * a.cap + k + li, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t wb = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.wtab) + k + li, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+      sw[li] = __longlong_as_double(static_cast<long long>(wb));
+    }
+    __syncthreads();
+    auto client = [&](int i) -> gptr<const T> {
+      const uint64_t p = sp[i];
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p));
+      const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p >> 32));
+      return to_global<T>(reinterpret_cast<const void*>(((static_cast<uint64_t>(hi) << 32) | lo) + elem_off));
+    };
+    if (full) {
+      // groups of CU_LOADS clients, every load of a group issued before its fold (tile_body)
+      for (int g = 0; g < n; g += CU_LOADS) {
+        V buf[CU_LOADS][VPL];
+        double wk[CU_LOADS];
+#pragma unroll
+        for (int c = 0; c < CU_LOADS; ++c) {
+          const int kc = min(g + c, n - 1);  // a short last group re-loads its last client
+          wk[c] = sw[kc];
+          LL::load_raw(client(kc), li, buf[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < CU_LOADS; ++c) {
+          const bool use = g + c < n;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) {
+            double x[N];
+            expand<T>(buf[c][v], x);
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+              double& r = acc[v * N + j];
+              const double nv = fold<FOLD_MULADD>(r, x[j], wk[c], 0.0);
+              r = use ? nv : r;
+            }
+          }
+        }
+      }
+    } else {
+      for (int i = 0; i < n; ++i) {
+        const double wk = sw[i];
+        double x[AE];
+        LC::load_checked(client(i), li, count, x);
+#pragma unroll
+        for (int j = 0; j < AE; ++j) acc[j] = fold<FOLD_MULADD>(acc[j], x[j], wk, 0.0);
+      }
+    }
+    k += n;
+    __syncthreads();  // sp / sw are refilled by the next batch
+  }
+
+  // the close: the mode, and for a final close the segment's divisor and output
+  if (threadIdx.x == 0) {
+    const int mode = static_cast<int>(dyn_ld_agent(&mir->mode));
+    s_mode = mode;
+    if (mode != OUT_ACC) {
+      s_W = __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+          reinterpret_cast<const uint64_t*>(a.wtot) + seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
+      s_out = __hip_atomic_load(a.outs + seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  const int mode = __builtin_amdgcn_readfirstlane(s_mode);
+  bool bad_acc = false;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = (v * LANES + li) * N;
+#pragma unroll
+    for (int j = 0; j < N; ++j) bad_acc |= (full || e + j < count) && (acc[v * N + j] != acc[v * N + j]);
+  }
+  if (mode == OUT_ACC) {
+    if (k == 0) return;  // nothing folded: the accumulator holds nothing for this round
+    const gptr<double> ap = to_global_mut<double>(a.acc + acc_base);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+#pragma unroll
+      for (int j = 0; j < N; j += 2) {
+        if (full || e + j + 2 <= count) {
+          store_out((gptr<f64x2>)(ap + e + j), f64x2{acc[v * N + j], acc[v * N + j + 1]});
+        } else {
+          if (e + j < count) ap[e + j] = acc[v * N + j];
+          if (e + j + 1 < count) ap[e + j + 1] = acc[v * N + j + 1];
+        }
+      }
+    }
+    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) raise_flag(a.flag, 0);
+    return;
+  }
+  // final close: the fused divide (_apply_total_weight, :71-74) and the :93 / :97 checks
+  double res[AE];
+  exact_div_block<AE>(acc, res, s_W);
+  bool bad_res = false;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = (v * LANES + li) * N;
+#pragma unroll
+    for (int j = 0; j < N; ++j) bad_res |= (full || e + j < count) && (res[v * N + j] != res[v * N + j]);
+  }
+  void* const out_raw = reinterpret_cast<void*>(s_out);
+  if (mode == OUT_F32) {
+    const gptr<float> op = to_global_mut<float>(out_raw) + td.start;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (full || e + j < count) op[e + j] = static_cast<float>(res[v * N + j]);
+    }
+  } else {
+    const gptr<double> op = to_global_mut<double>(out_raw) + td.start;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int e = (v * LANES + li) * N;
+#pragma unroll
+      for (int j = 0; j < N; j += 2) {
+        if (full || e + j + 2 <= count) {
+          store_out((gptr<f64x2>)(op + e + j), f64x2{res[v * N + j], res[v * N + j + 1]});
+        } else {
+          if (e + j < count) op[e + j] = res[v * N + j];
+          if (e + j + 1 < count) op[e + j + 1] = res[v * N + j + 1];
+        }
+      }
+    }
+  }
+  const uint64_t ba = __ballot(bad_acc);
+  const uint64_t br = __ballot(bad_res);
+  if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+    if (ba) raise_flag(a.flag, 0);
+    if (br) raise_flag(a.flag, 1);
   }
 }
 
@@ -1716,11 +2028,42 @@ struct fedavg_ctx {
   size_t qtab_last_bytes = 0;                // table bytes of the last QSGD launch
   hipEvent_t aux_done = nullptr;  // the last upload out of aux_host finished
   bool aux_used = false;
+  // the dynamic wave (fedavg_dyn_*): its host-coherent control block and row table, the device
+  // mirror words, a private stream (the caller's stream stays free for the work producing the
+  // arrivals) and the per-segment totals of the published rows
+  struct Dyn {
+    bool active = false;
+    int32_t in_dtype = -1;
+    int32_t published = 0;
+    int32_t cap = 0;
+    char* host = nullptr;      // DynCtl, DynAck, wtot[T], outs[T], wtab[cap], ptab[T][cap]
+    char* dev_alias = nullptr;
+    size_t bytes = 0;
+    char* mirror = nullptr;    // kDynCopies DynMirror (device)
+    hipStream_t stream = nullptr;
+    hipEvent_t start = nullptr, done = nullptr;
+    std::vector<double> wsum;  // per segment, the published rows' weights in arrival order
+    uint64_t idle_ticks = 0, life_ticks = 0;
+  } dyn;
 };
 
 namespace {
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct DynLayout {  // offsets into the host-coherent block
+  size_t ctl, ack, wtot, outs, wtab, ptab, bytes;
+  DynLayout(int T, int cap) {
+    ctl = 0;
+    ack = align_up(ctl + sizeof(DynCtl), 64);
+    wtot = align_up(ack + sizeof(DynAck), 64);
+    outs = align_up(wtot + sizeof(double) * T, 64);
+    wtab = align_up(outs + sizeof(uint64_t) * T, 64);
+    ptab = align_up(wtab + sizeof(double) * cap, 64);
+    bytes = align_up(ptab + sizeof(uint64_t) * static_cast<size_t>(T) * cap, 4096);
+  }
+};
+
 
 int32_t elem_size(int32_t dt) {
   switch (dt) {
@@ -2176,6 +2519,8 @@ int32_t launch_main(fedavg_ctx* c, hipStream_t s, const Staged& st, int32_t in_d
                     int split, int32_t zero_init, int32_t tb_split1, int32_t te_split1,
                     hipEvent_t* done_ev = nullptr, double* acc_out = nullptr,
                     const KArgs* win = nullptr, const KArgs* comb = nullptr) {
+  if (c->dyn.active)
+    return fail(FEDAVG_ERR_STATE, "a dynamic wave is open on this context (fedavg_dyn_close it first)");
   if (st.delta) split = 1;  // delta folds run the exact-order kernel only
   if (comb) split = 1;
   KArgs a;
@@ -2608,7 +2953,21 @@ int32_t fedavg_ctx_create(fedavg_ctx** out, int32_t device, const int64_t* seg_n
 int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   if (c == nullptr) return FEDAVG_OK;
   (void)hipSetDevice(c->device);
+  if (c->dyn.active) {
+    // an open dynamic wave ends with the rows it has (its ACK arrives within a mirror poll)
+    const DynLayout L(c->T, c->dyn.cap);
+    DynCtl* ctl = reinterpret_cast<DynCtl*>(c->dyn.host + L.ctl);
+    __atomic_store_n(&ctl->mode, static_cast<uint32_t>(OUT_ACC), __ATOMIC_RELAXED);
+    __atomic_store_n(&ctl->closed, 1u, __ATOMIC_RELEASE);
+    c->dyn.active = false;
+  }
+  if (c->dyn.stream) (void)hipStreamSynchronize(c->dyn.stream);
   (void)hipDeviceSynchronize();
+  if (c->dyn.host) (void)hipHostFree(c->dyn.host);
+  if (c->dyn.mirror) (void)hipFree(c->dyn.mirror);
+  if (c->dyn.start) (void)hipEventDestroy(c->dyn.start);
+  if (c->dyn.done) (void)hipEventDestroy(c->dyn.done);
+  if (c->dyn.stream) (void)hipStreamDestroy(c->dyn.stream);
   for (auto& sl : c->slots) {
     if (sl.host) (void)hipHostFree(sl.host);
     if (sl.dev) (void)hipFree(sl.dev);
@@ -2657,9 +3016,16 @@ int32_t fedavg_set_fused_fold(fedavg_ctx* c, int32_t enable) {
   return FEDAVG_OK;
 }
 
+int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, void* stream, int32_t* folded_out,
+                         int32_t* finalized_out);
+
 int32_t fedavg_reset(fedavg_ctx* c, void* stream) {
   FEDAVG_RET(check_ctx(c));
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  if (c->dyn.active) {  // an abandoned round's dynamic wave: ended and drained before the reset
+    FEDAVG_RET(fedavg_dyn_close(c, nullptr, FEDAVG_F64, stream, nullptr, nullptr));
+    FEDAVG_HIP_TRY(hipStreamSynchronize(c->dyn.stream));
+  }
   std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -3497,6 +3863,222 @@ int32_t fedavg_bw_probe(const void* src, int64_t bytes, void* dst, int32_t mode,
                        static_cast<uint32_t*>(dst), n);
   }
   FEDAVG_HIP_TRY(hipGetLastError());
+  return FEDAVG_OK;
+}
+
+}  // extern "C"
+
+// ---- dynamic waves (dyn_wave_kernel) ------------------------------------------------------
+namespace {
+
+uint64_t dyn_env_us(const char* name, uint64_t dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
+}
+
+int32_t dyn_wait_ack(fedavg_ctx* c, uint32_t* state, uint32_t* count) {
+  const DynLayout L(c->T, c->dyn.cap);
+  const DynAck* ack = reinterpret_cast<const DynAck*>(c->dyn.host + L.ack);
+  // the mirror answers within a poll (~1 µs); a wave whose mirror never runs is ended by its
+  // own lifetime limit, so this wait is bounded by that (plus a margin)
+  const auto t0 = std::chrono::steady_clock::now();
+  const double limit_s = static_cast<double>(c->dyn.life_ticks) / 1e8 + 5.0;
+  for (;;) {
+    const uint32_t st = __atomic_load_n(&ack->state, __ATOMIC_ACQUIRE);
+    if (st != 0) {
+      *state = st;
+      *count = __atomic_load_n(&ack->count, __ATOMIC_ACQUIRE);
+      return FEDAVG_OK;
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+      return fail(FEDAVG_ERR_HIP, "the dynamic wave did not acknowledge its close");
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, void* stream) {
+  FEDAVG_RET(check_ctx(c));
+  auto& d = c->dyn;
+  if (d.active) return fail(FEDAVG_ERR_STATE, "a dynamic wave is already open");
+  if (in_dtype != FEDAVG_F32 && in_dtype != FEDAVG_F16 && in_dtype != FEDAVG_BF16 && in_dtype != FEDAVG_F64)
+    return fail(FEDAVG_ERR_INVALID, "dynamic waves take fp32 / fp16 / bf16 / fp64 inputs");
+  if (max_clients < 1) return fail(FEDAVG_ERR_INVALID, "max_clients must be >= 1");
+  for (int t = 0; t < c->T; ++t)
+    if (c->valid[t]) return fail(FEDAVG_ERR_STATE, "a dynamic wave opens a round: the accumulator already holds data");
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  if (!d.stream) {
+    FEDAVG_HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.start, hipEventDisableTiming));
+    FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.mirror), sizeof(DynMirror) * kDynCopies));
+    d.idle_ticks = dyn_env_us("FEDAVG_DYN_IDLE_US", 500) * 100;      // s_memrealtime: 100 MHz
+    d.life_ticks = dyn_env_us("FEDAVG_DYN_LIFE_US", 2000000) * 100;
+  }
+  if (d.cap < max_clients) {
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));  // the previous wave has left the old block
+    if (d.host) FEDAVG_HIP_TRY(hipHostFree(d.host));
+    d.host = nullptr;
+    d.cap = 0;
+    const int cap = std::max(max_clients, 64);
+    const DynLayout L(c->T, cap);
+    FEDAVG_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.host), L.bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    FEDAVG_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d.dev_alias), d.host, 0));
+    d.cap = cap;
+    d.bytes = L.bytes;
+  }
+  FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));  // the previous wave read its block to the end
+  const DynLayout L(c->T, d.cap);
+  DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
+  DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);
+  __atomic_store_n(&ctl->count, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&ctl->closed, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&ctl->mode, static_cast<uint32_t>(OUT_ACC), __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->state, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->count, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->error, 0u, __ATOMIC_RELEASE);
+  d.wsum.assign(c->T, -0.0);
+  d.published = 0;
+  d.in_dtype = in_dtype;
+  // the wave starts behind the caller's stream (what it enqueued so far), on the private stream
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  FEDAVG_HIP_TRY(hipEventRecord(d.start, s));
+  FEDAVG_HIP_TRY(hipStreamWaitEvent(d.stream, d.start, 0));
+  FEDAVG_HIP_TRY(hipMemsetAsync(d.mirror, 0, sizeof(DynMirror) * kDynCopies, d.stream));
+  DynArgs a{};
+  a.tiles = c->d_tiles1;
+  a.segs = c->d_segs;
+  a.acc = c->acc;
+  a.flag = c->d_flag;
+  a.ctl = reinterpret_cast<DynCtl*>(d.dev_alias + L.ctl);
+  a.ack = reinterpret_cast<DynAck*>(d.dev_alias + L.ack);
+  a.wtot = reinterpret_cast<const double*>(d.dev_alias + L.wtot);
+  a.outs = reinterpret_cast<const uint64_t*>(d.dev_alias + L.outs);
+  a.wtab = reinterpret_cast<const double*>(d.dev_alias + L.wtab);
+  a.ptab = reinterpret_cast<const uint64_t*>(d.dev_alias + L.ptab);
+  a.mir = reinterpret_cast<DynMirror*>(d.mirror);
+  a.num_tiles = static_cast<int32_t>(c->tiles1.size());
+  a.cap = d.cap;
+  a.idle_ticks = d.idle_ticks;
+  a.life_ticks = d.life_ticks;
+  const dim3 grid(static_cast<unsigned>(a.num_tiles + 1));
+  switch (in_dtype) {
+    case FEDAVG_F32: hipLaunchKernelGGL(dyn_wave_kernel<float>, grid, dim3(Geo<float, 1, kTile1>::THREADS), 0, d.stream, a); break;
+    case FEDAVG_F16: hipLaunchKernelGGL(dyn_wave_kernel<__half>, grid, dim3(Geo<__half, 1, kTile1>::THREADS), 0, d.stream, a); break;
+    case FEDAVG_BF16: hipLaunchKernelGGL(dyn_wave_kernel<bf16_t>, grid, dim3(Geo<bf16_t, 1, kTile1>::THREADS), 0, d.stream, a); break;
+    default: hipLaunchKernelGGL(dyn_wave_kernel<double>, grid, dim3(Geo<double, 1, kTile1>::THREADS), 0, d.stream, a); break;
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  d.active = true;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_publish(fedavg_ctx* c, const void* const* client_ptrs, const double* weights, int32_t K,
+                           void* stream, int32_t* published_out) {
+  FEDAVG_RET(check_ctx(c));
+  auto& d = c->dyn;
+  if (published_out) *published_out = 0;
+  if (!d.active) return fail(FEDAVG_ERR_STATE, "no dynamic wave is open");
+  if (K < d.published || K > d.cap) return fail(FEDAVG_ERR_INVALID, "row count outside the wave's table");
+  if (K == d.published) return FEDAVG_OK;
+  const int T = c->T;
+  // rows the wave can take: every tensor present, 16-B aligned, one weight per row
+  for (int k = d.published; k < K; ++k) {
+    const double w = weights[static_cast<int64_t>(k) * T];
+    for (int t = 0; t < T; ++t) {
+      const void* p = client_ptrs[static_cast<int64_t>(k) * T + t];
+      const double wt = weights[static_cast<int64_t>(k) * T + t];
+      if (!p || reinterpret_cast<uintptr_t>(p) % 16 != 0 || std::memcmp(&wt, &w, sizeof(double)) != 0)
+        return fail(FEDAVG_ERR_INVALID, "a row the dynamic wave cannot take (absent / unaligned tensor, per-tensor weights)");
+    }
+  }
+  // the caller's stream must have finished what it enqueued: the arrivals' tensors are then
+  // complete (the wave runs on its own stream); otherwise nothing is published now
+  if (hipStreamQuery(static_cast<hipStream_t>(stream)) != hipSuccess) return FEDAVG_OK;
+  const DynLayout L(T, d.cap);
+  uint64_t* ptab = reinterpret_cast<uint64_t*>(d.host + L.ptab);
+  double* wtab = reinterpret_cast<double*>(d.host + L.wtab);
+  for (int k = d.published; k < K; ++k) {
+    const double w = weights[static_cast<int64_t>(k) * T];
+    wtab[k] = w;
+    for (int t = 0; t < T; ++t) {
+      ptab[static_cast<int64_t>(t) * d.cap + k] =
+          reinterpret_cast<uint64_t>(client_ptrs[static_cast<int64_t>(k) * T + t]);
+      d.wsum[t] += w;  // fed_avg_algorithm.py:59-62, arrival order
+    }
+  }
+  DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
+  __atomic_store_n(&ctl->count, static_cast<uint32_t>(K), __ATOMIC_RELEASE);
+  if (published_out) *published_out = K - d.published;
+  d.published = K;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, void* stream, int32_t* folded_out,
+                         int32_t* finalized_out) {
+  FEDAVG_RET(check_ctx(c));
+  auto& d = c->dyn;
+  if (!d.active) return fail(FEDAVG_ERR_STATE, "no dynamic wave is open");
+  const int T = c->T;
+  const DynLayout L(T, d.cap);
+  DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
+  uint32_t mode = OUT_ACC;
+  if (out_ptrs && d.published > 0) {
+    const int ok = out_kind_of(out_dtype);
+    if (ok < 0) return fail(FEDAVG_ERR_INVALID, "out dtype must be FEDAVG_F32 or FEDAVG_F64");
+    bool aligned = true;
+    for (int t = 0; t < T; ++t) aligned = aligned && out_ptrs[t] && reinterpret_cast<uintptr_t>(out_ptrs[t]) % 16 == 0;
+    if (aligned) {  // (unaligned outputs: the wave stores the accumulator, the caller divides)
+      double* wtot = reinterpret_cast<double*>(d.host + L.wtot);
+      uint64_t* outs = reinterpret_cast<uint64_t*>(d.host + L.outs);
+      for (int t = 0; t < T; ++t) {
+        wtot[t] = d.wsum[t];
+        outs[t] = reinterpret_cast<uint64_t>(out_ptrs[t]);
+      }
+      mode = static_cast<uint32_t>(ok);
+    }
+  }
+  __atomic_store_n(&ctl->mode, mode, __ATOMIC_RELAXED);
+  __atomic_store_n(&ctl->closed, 1u, __ATOMIC_RELEASE);
+  uint32_t state = 0, folded = 0;
+  FEDAVG_RET(dyn_wait_ack(c, &state, &folded));
+  d.active = false;
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  FEDAVG_HIP_TRY(hipEventRecord(d.done, d.stream));
+  FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.done, 0));
+  const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
+  if (__atomic_load_n(&ack->error, __ATOMIC_ACQUIRE)) {
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
+    std::fill(c->valid.begin(), c->valid.end(), 0);
+    return fail(FEDAVG_ERR_HIP, "a dynamic wave's workgroup lost its mirror (the wave's results are invalid)");
+  }
+  const bool finalized = state == 1 && mode != OUT_ACC;
+  if (finalized) {
+    fedavg_internal_clear_state(c);  // the round's result is written (fed_avg_algorithm.py:90,98)
+  } else if (folded > 0) {
+    // the accumulator holds rows [0, folded): their totals, in arrival order
+    const double* wtab = reinterpret_cast<const double*>(d.host + L.wtab);
+    for (int t = 0; t < T; ++t) {
+      double s = -0.0;
+      for (uint32_t k = 0; k < folded; ++k) s += wtab[k];
+      c->wsum[t] = s;
+      c->valid[t] = 1;
+    }
+  }
+  if (folded_out) *folded_out = static_cast<int32_t>(folded);
+  if (finalized_out) *finalized_out = finalized ? 1 : 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_state(const fedavg_ctx* c, int32_t* active, int32_t* published) {
+  FEDAVG_RET(check_ctx(c));
+  if (active) *active = c->dyn.active ? 1 : 0;
+  if (published) *published = c->dyn.published;
   return FEDAVG_OK;
 }
 

@@ -653,6 +653,33 @@ class FedAvgContext:
     def reset(self) -> None:
         _native.check(self._lib.fedavg_reset(self._h, self.stream))
 
+    # -- dynamic waves (fedavg_dyn_*: the round's first wave folded while clients arrive) -
+    def dyn_open(self, in_dtype: torch.dtype, max_clients: int) -> None:
+        _native.check(self._lib.fedavg_dyn_open(self._h, dtype_code(in_dtype), int(max_clients), self.stream))
+
+    def dyn_publish(self, table: ClientTable) -> int:
+        """Hand the table's unpublished rows to the open wave; the rows published now (0 while
+        the current stream still has unfinished work). NativeError for rows the wave cannot take."""
+        p, w = _table_args(table)
+        n = ctypes.c_int32()
+        _native.check(self._lib.fedavg_dyn_publish(self._h, p, w, table.num_clients, self.stream, ctypes.byref(n)))
+        return int(n.value)
+
+    def dyn_close(self, outs: Sequence[torch.Tensor] | OutputTable | None = None,
+                  out_dtype: torch.dtype = torch.float64) -> tuple[int, bool]:
+        """(rows folded, finalized): with ``outs`` the wave divides into them (finalized), else —
+        or when it ended itself — it leaves rows [0, folded) in the accumulator."""
+        ot = self._out_table(outs, out_dtype) if outs is not None else None
+        folded, fin = ctypes.c_int32(), ctypes.c_int32()
+        _native.check(self._lib.fedavg_dyn_close(self._h, ot, out_code(out_dtype), self.stream, ctypes.byref(folded),
+                                                 ctypes.byref(fin)))
+        return int(folded.value), bool(fin.value)
+
+    def dyn_state(self) -> tuple[bool, int]:
+        a, p = ctypes.c_int32(), ctypes.c_int32()
+        _native.check(self._lib.fedavg_dyn_state(self._h, ctypes.byref(a), ctypes.byref(p)))
+        return bool(a.value), int(p.value)
+
     # -- fault reporting ---------------------------------------------------------------
     def flags(self) -> int:
         """Synchronise the stream and return the latched NaN flag bits."""

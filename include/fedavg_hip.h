@@ -447,6 +447,41 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
                                    void* stream);
 
 /* =====================================================================================
+ * Dynamic waves — the round's first wave folded while its clients still arrive.
+ * Replaces, for the plugin's round (FedAVGAlgorithm.process_worker_data x N then
+ * aggregate_worker_data, simulation_lib/algorithm/fed_avg_algorithm.py:20-113, driven by
+ * simulation_lib/server/aggregation_server.py:111-145), the wave that could only start once every
+ * arrival was staged: the kernel is launched at the first arrival with an open client count.
+ *
+ *   fedavg_dyn_open(ctx, in_dtype, max_clients, stream)
+ *       launch the wave (zero-initialised: the accumulator must hold nothing yet) on a private
+ *       stream, behind what `stream` holds so far. While it is open every other launch on the
+ *       context fails with FEDAVG_ERR_STATE.
+ *   fedavg_dyn_publish(ctx, client_ptrs[K][T], weights[K][T], K, stream, &published)
+ *       hand rows [already published, K) of the caller's client table to the wave (rows keep
+ *       their indices: the same table the caller appends to). Rows must carry every tensor, 16-B
+ *       aligned, one weight per row (else FEDAVG_ERR_INVALID: close the wave and fold the rest
+ *       the ordinary way). Nothing is published (published = 0) while `stream` has unfinished
+ *       work — the tensors of those rows may not be written yet.
+ *   fedavg_dyn_close(ctx, out_ptrs or NULL, out_dtype, stream, &folded, &finalized)
+ *       fix the count. With out_ptrs (16-B aligned) the wave divides by the published rows'
+ *       totals (arrival order) into the outputs: finalized = 1, the round is done (check with
+ *       fedavg_check on `stream`). Otherwise — NULL outputs, or the wave ended itself after
+ *       FEDAVG_DYN_IDLE_US (500) µs without a new row or FEDAVG_DYN_LIFE_US (2 s) in all — it
+ *       stores the fp64 accumulator of rows [0, folded) (the context's state says so) and the
+ *       caller folds rows [folded, K) with the ordinary calls. `stream` continues after the wave.
+ *   fedavg_dyn_state(ctx, &active, &published)
+ * Per element the fold is the reference's arrival-order chain (separately rounded product and
+ * sum): the bits equal fedavg_aggregate's.
+ * ===================================================================================== */
+int32_t fedavg_dyn_open(fedavg_ctx* ctx, int32_t in_dtype, int32_t max_clients, void* stream);
+int32_t fedavg_dyn_publish(fedavg_ctx* ctx, const void* const* client_ptrs, const double* weights, int32_t num_clients,
+                           void* stream, int32_t* published_out);
+int32_t fedavg_dyn_close(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dtype, void* stream, int32_t* folded_out,
+                         int32_t* finalized_out);
+int32_t fedavg_dyn_state(const fedavg_ctx* ctx, int32_t* active, int32_t* published);
+
+/* =====================================================================================
  * Single-process multi-device mode ("a communicator created by the library
  * from a device list"). The reference drives aggregation from ONE server process
  * (simulation_lib/server/server.py:122-152 -> aggregation_server.py:111-145 ->

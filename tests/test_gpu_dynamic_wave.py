@@ -1,0 +1,190 @@
+"""The dynamic wave (include/fedavg_hip.h fedavg_dyn_*): the plugin round's first wave folded while
+its clients arrive, on the MI355X.
+
+Every result is asserted BIT-IDENTICAL to the oracle's arrival-order chain (fed_avg_algorithm.py:
+43-99): whether the wave divides into the outputs itself, is closed early (a row it cannot take, a
+busy stream, its own idle limit) and leaves the ordinary waves the rest, or is abandoned.
+"""
+
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_learning_simulation_lib_amd import FedAVGAlgorithm, ParameterMessage, _native
+from distributed_learning_simulation_lib_amd._staging import NativeClientTable
+from distributed_learning_simulation_lib_amd.fedavg import FedAvgContext, ModelLayout, NaNAggregationError, OutputTable
+from oracle.fedavg_oracle import OracleFedAvg, OracleMessage
+from tests.golden_io import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {"conv": (16, 3, 5, 5), "bias": (16,), "fc": (10, 700), "big": (3, 4096), "tail": (4096 + 37,)}
+
+
+def _round(algo, dev, n, seed, dtype=torch.float32, weights="int", mutate=None):
+    g = torch.Generator().manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    oracle = OracleFedAvg()
+    for k in range(n):
+        p = {name: torch.randn(s, generator=g).to(dtype) for name, s in SHAPES.items()}
+        if mutate is not None:
+            p = mutate(k, p)
+        w = int(rng.integers(100, 5000)) if weights == "int" else float(rng.uniform(0.1, 3.0))
+        algo.process_worker_data(k, ParameterMessage(parameter={m: t.to(dev) for m, t in p.items()},
+                                                     aggregation_weight=w))
+        arrs = {m: (t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy())
+                for m, t in p.items()}
+        oracle.process_worker_data(k, OracleMessage(parameter=arrs, aggregation_weight=w,
+                                                    dtype="bfloat16" if dtype == torch.bfloat16 else None))
+    got = algo.aggregate_worker_data().parameter
+    algo.clear_worker_data()
+    want = oracle.aggregate_worker_data().parameter
+    assert list(got) == list(want)
+    for name, v in want.items():
+        g_ = got[name]
+        if algo.result_dtype == torch.float32:
+            assert torch.equal(g_.cpu(), torch.from_numpy(v).to(torch.float32)), name
+        else:
+            assert bits_equal(g_.cpu().numpy(), v), name
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16, torch.float64])
+@pytest.mark.parametrize("n,wave", [(1, 64), (3, 64), (9, 64), (64, 64), (10, 4), (13, 13)])
+def test_plugin_rounds_bit_identical(hip_device, dtype, n, wave):
+    algo = FedAVGAlgorithm(device=hip_device, wave_size=wave, dynamic_wave=True)
+    for r in range(2):  # two rounds on one object: the wave reopens every round
+        _round(algo, hip_device, n, 10 * n + r, dtype)
+    algo.exit()
+
+
+@pytest.mark.parametrize("result_dtype", [torch.float32, torch.float64])
+def test_fractional_weights_and_result_dtypes(hip_device, result_dtype):
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True, result_dtype=result_dtype)
+    _round(algo, hip_device, 11, 5, weights="float")
+    algo.exit()
+
+
+def test_a_row_it_cannot_take_closes_it_early(hip_device):
+    # client 4 misses a tensor: the wave keeps clients 0-3, the ordinary waves fold 4-8
+    def mutate(k, p):
+        if k == 4:
+            del p["fc"]
+        return p
+
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    _round(algo, hip_device, 9, 21, mutate=mutate)
+    algo.exit()
+
+
+def test_busy_stream_defers_publication(hip_device):
+    # the current stream holds unfinished work at every arrival: nothing is published before the
+    # close (which waits for the stream), results unchanged
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+
+    def mutate(k, p):
+        torch.cuda._sleep(2_000_000)  # ~1 ms of GPU work on the current stream
+        return p
+
+    _round(algo, hip_device, 6, 22, mutate=mutate)
+    algo.exit()
+
+
+def test_wave_ends_itself_when_arrivals_stop(hip_device, monkeypatch):
+    # FEDAVG_DYN_IDLE_US=200: a 30 ms gap between arrivals ends the wave with the rows it has;
+    # the later rows go through the ordinary waves
+    monkeypatch.setenv("FEDAVG_DYN_IDLE_US", "200")
+    monkeypatch.setenv("FEDAVG_DYN_BATCH", "1")
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+
+    def mutate(k, p):
+        if k == 3:
+            torch.cuda.synchronize()
+            time.sleep(0.03)
+        return p
+
+    _round(algo, hip_device, 8, 23, mutate=mutate)
+    algo.exit()
+
+
+def test_nan_input_names_the_client(hip_device):
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    g = torch.Generator().manual_seed(3)
+    for k in range(5):
+        p = {name: torch.randn(s, generator=g) for name, s in SHAPES.items()}
+        if k == 2:
+            p["fc"][3, 7] = float("nan")
+        algo.process_worker_data(k, ParameterMessage(parameter={m: t.to(hip_device) for m, t in p.items()},
+                                                     aggregation_weight=10 + k))
+    with pytest.raises(NaNAggregationError) as ei:
+        algo.aggregate_worker_data()
+    assert ei.value.stage == "input" and ei.value.bad_clients == [2]
+    algo.clear_worker_data()
+    _round(algo, hip_device, 4, 24)  # the object is usable afterwards
+    algo.exit()
+
+
+def test_abandoned_round_and_exit_with_an_open_wave(hip_device):
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    g = torch.Generator().manual_seed(4)
+    for k in range(3):
+        p = {name: torch.randn(s, generator=g).to(hip_device) for name, s in SHAPES.items()}
+        algo.process_worker_data(k, ParameterMessage(parameter=p, aggregation_weight=1 + k))
+    algo.clear_worker_data()  # the round is dropped with its wave open
+    _round(algo, hip_device, 5, 25)
+    for k in range(2):
+        p = {name: torch.randn(s, generator=g).to(hip_device) for name, s in SHAPES.items()}
+        algo.process_worker_data(k, ParameterMessage(parameter=p, aggregation_weight=1 + k))
+    algo.exit()  # the context is destroyed with a wave open
+    assert float(torch.ones(4, device=hip_device).sum().item()) == 4.0
+
+
+def test_c_abi_protocol(hip_device):
+    """open / publish / close directly: other launches are refused while the wave is open, an
+    accumulator close leaves rows [0, folded) for the ordinary calls, a final close divides."""
+    layout = ModelLayout.flat(10_000)
+    ctx = FedAvgContext(layout, hip_device)
+    g = torch.Generator().manual_seed(6)
+    xs = [torch.randn(10_000, generator=g) for _ in range(7)]
+    ws = [float(3 + k) for k in range(7)]
+    table = NativeClientTable(1, hip_device.index or 0)
+    dev = [x.to(hip_device) for x in xs]
+    for x, w in zip(dev, ws):
+        table.add_client([x], [w])
+    want = OracleFedAvg()
+    for k, (x, w) in enumerate(zip(xs, ws)):
+        want.process_worker_data(k, OracleMessage(parameter={"bucket": x.numpy()}, aggregation_weight=w))
+    want = want.aggregate_worker_data().parameter["bucket"]
+    out = torch.empty(10_000, dtype=torch.float64, device=hip_device)
+    outs = OutputTable([out], layout, hip_device, torch.float64)
+    try:
+        ctx.dyn_open(torch.float32, 16)
+        assert ctx.dyn_state() == (True, 0)
+        with pytest.raises(_native.NativeError):
+            ctx.accumulate(table, torch.float32)  # refused while the wave is open
+        torch.cuda.synchronize(hip_device)
+        assert ctx.dyn_publish(table) == 7
+        folded, fin = ctx.dyn_close(outs, torch.float64)
+        assert (folded, fin) == (7, True)
+        ctx.raise_on_nan()
+        assert bits_equal(out.cpu().numpy(), want)
+        # accumulator close after 4 rows, the rest by the ordinary call
+        from distributed_learning_simulation_lib_amd._staging import TableTail
+
+        head = NativeClientTable(1, hip_device.index or 0)
+        for x, w in zip(dev[:4], ws[:4]):
+            head.add_client([x], [w])
+        ctx.dyn_open(torch.float32, 16)
+        torch.cuda.synchronize(hip_device)
+        assert ctx.dyn_publish(head) == 4
+        assert ctx.dyn_close(None) == (4, False)
+        out.fill_(float("nan"))
+        ctx.aggregate(TableTail(table, 4), torch.float32, outs, torch.float64)
+        ctx.raise_on_nan()
+        assert bits_equal(out.cpu().numpy(), want)
+        ctx.reset()
+    finally:
+        ctx.close()

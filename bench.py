@@ -1047,6 +1047,7 @@ def main_plugin(args: argparse.Namespace) -> int:
     ctx.prof_collect()
     ctx.prof_enable(not args.no_kernel_events)
     host_s[0] = 0.0
+    dyn0 = dict(algo.dyn_stats)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -1055,6 +1056,7 @@ def main_plugin(args: argparse.Namespace) -> int:
     elapsed = time.perf_counter() - t0
     ctx.prof_enable(False)
     kernel_ms, launches = ctx.prof_collect()
+    dyn = {k: round((algo.dyn_stats[k] - dyn0[k]) / args.steps, 2) for k in dyn0}
     in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
     job_bytes = N * P * in_b + P * out_b
     n_waves = -(-N // wave)
@@ -1090,6 +1092,10 @@ def main_plugin(args: argparse.Namespace) -> int:
                    "clients": N, "params_per_client": P, "tensors_per_client": T, "in_dtype": args.in_dtype,
                    "out_dtype": args.out_dtype, "clients_per_launch": wave, "wave_min": algo.wave_min,
                    "waves_per_round": round(launches / args.steps, 2) if launches else None, "in_round": in_round,
+                   # the round's first wave folded during the arrivals (fedavg_dyn_*):
+                   # rows it folded and rounds it divided itself, per round; its kernel spans the
+                   # arrival phase, so the event timing and roofline below cover the ordinary waves only
+                   "dynamic_wave": dict(dyn, enabled=algo.dynamic_wave),
                    "host_us_per_update": round(host_s[0] / (args.steps * N) * 1e6, 2),
                    "process_worker_data_ms_per_round": round(host_s[0] / args.steps * 1e3, 4),
                    # what a round costs beyond its kernels: staging, launch, NaN readback, result dict

@@ -160,6 +160,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__dyn_pub = 0                   # its rows published so far
         self.__dyn_closed: Any = None        # (table, rows folded) of the round's closed dynamic wave
         self.__dyn_round = False             # the round's first wave has been decided
+        # dynamic waves opened, rows they folded, waves that wrote the round's result themselves
+        self.dyn_stats = {"waves": 0, "rows": 0, "finalized": 0}
         self.result_dtype = result_dtype
         self.result_device = torch.device(result_device) if result_device is not None else None
         self.split_policy = split_policy
@@ -936,6 +938,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             except _native.NativeError:
                 return  # e.g. the accumulator already holds data: the ordinary waves
             self.__dyn_table, self.__dyn_pub, self.__dyn_closed = table, 0, None
+            self.dyn_stats["waves"] += 1
         elif self.__dyn_table is not table:
             return
         if table.num_clients - self.__dyn_pub >= self.__dyn_batch:
@@ -956,6 +959,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__dyn_table = None
         folded, finalized = self._context().dyn_close(outs, out_dtype)
         self.__dyn_closed = (table, folded)
+        self.dyn_stats["rows"] += folded
+        self.dyn_stats["finalized"] += int(finalized)
         return finalized
 
     def _dyn_rest(self, table: Any) -> Any:

@@ -861,13 +861,22 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS)) void fedavg_tile_k
 // acc + round(x * w) per client in arrival order — so the bits are those of the one-launch
 // kernel.
 //
-// Workgroup 0 is the mirror: one thread polls the host control words over PCIe and republishes
-// the row count in device memory, so the tile workgroups poll device memory only; it also ends
-// the wave by itself (state 2, accumulator mode) when the host publishes nothing for `idle`
-// ticks or the wave outlives `life` ticks, and acknowledges every close in host memory — the
-// host learns from that acknowledgement how many rows were folded. Every workgroup leaves once
-// the mirror closed (tile workgroups also after `life` + a margin on their own): no wave spins
-// past the wave's lifetime. All stores are vector stores (global_store with scope bits).
+// Workgroup 0 is the mirror: its thread 0 polls the host control words over PCIe; on new rows
+// the whole workgroup copies them (client pointers, weights; at a final close the divisors and
+// output pointers) from the host table into a device table and then republishes the row count
+// in device memory, so the tile workgroups never read host memory and poll device memory only.
+// The mirror also ends the wave by itself (state 2, accumulator mode) when the host publishes
+// nothing for `idle` ticks or the wave outlives `life` ticks, and acknowledges every close in
+// host memory — the host learns from that acknowledgement how many rows were folded. Every
+// workgroup leaves once the mirror closed (tile workgroups also after `life` + a margin on their
+// own): no wave spins past the wave's lifetime.
+//
+// Hand-off inside the launch (cdna_hip_programming.md §6 Guideline 16): the device table is
+// written with system-coherent stores and read with system-coherent loads (no stale L1 / L2 copy
+// of a line a consumer read before its later rows were written); every storing wave of the mirror
+// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which ONE lane
+// publishes the count word (8-B agent-scope store); a tile workgroup polls that word relaxed and
+// needs no acquire (it reads no handed-off byte through L1 / L2). All stores are vector stores.
 struct DynCtl {     // host-coherent, written by the host
   uint32_t count;   // rows published (release)
   uint32_t closed;  // 1: `count` is final
@@ -881,95 +890,235 @@ struct DynAck {     // host-coherent, written by the mirror workgroup
   uint32_t pad;
 };
 struct DynMirror {  // device memory, written by the mirror workgroup: one copy per XCD (kDynCopies,
-  uint32_t count;   // a cache line apart), so the tile workgroups' polls spread over 8 lines
-  uint32_t closed;
-  uint32_t mode;
-  uint32_t pad[13];
+  uint64_t word;    // a cache line apart), so the tile workgroups' polls spread over 8 lines
+  uint64_t pad[7];
 };
 constexpr int kDynCopies = 8;
+// the mirror word: rows mirrored (bits 0-23), closed (bit 24), close mode (bits 25-27), the wave's
+// epoch (bits 32-63: a word left by an earlier wave reads as "nothing yet", so no per-wave reset)
+__host__ __device__ constexpr uint64_t dyn_word(uint32_t count, uint32_t closed, uint32_t mode, uint32_t epoch) {
+  return static_cast<uint64_t>(count & 0xffffffu) | (static_cast<uint64_t>(closed & 1u) << 24) |
+         (static_cast<uint64_t>(mode & 7u) << 25) | (static_cast<uint64_t>(epoch) << 32);
+}
 struct DynArgs {
-  const TileDesc* tiles;
+  const TileDesc* tiles;       // body tiles (kDynTile elements each)
+  const TileDesc* edge_tiles;  // edge tiles (<= kDynEdgeTile elements each)
   const SegDesc* segs;
   double* acc;
   uint32_t* flag;
   DynCtl* ctl;              // device aliases of the host-coherent block
   DynAck* ack;
-  const uint64_t* ptab;     // [T][cap] client pointers, segment-major
-  const double* wtab;       // [cap] client weights
-  const double* wtot;       // [T] divisors (final close)
-  const uint64_t* outs;     // [T] output pointers (final close)
+  const uint64_t* h_ptab;   // host table: [T][cap] client pointers, segment-major
+  const double* h_wtab;     // [cap] client weights
+  const double* h_wtot;     // [T] divisors (final close)
+  const uint64_t* h_outs;   // [T] output pointers (final close)
+  uint64_t* ptab;           // the device copies the mirror writes
+  double* wtab;
+  double* wtot;
+  uint64_t* outs;
   DynMirror* mir;
   int32_t num_tiles;
+  int32_t num_segs;
   int32_t cap;
+  uint32_t epoch;
   uint64_t idle_ticks;      // s_memrealtime ticks (100 MHz)
   uint64_t life_ticks;
 };
 
 constexpr int kDynBatch = 64;  // rows a tile workgroup fetches per poll (one per lane of wave 0)
 
-__device__ __forceinline__ uint32_t dyn_ld_sys(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint32_t dyn_ld_host(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint32_t dyn_ld_agent(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint64_t dyn_ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void dyn_st_sys64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double dyn_ld_sysf(const double* p) {
+  return __longlong_as_double(static_cast<long long>(dyn_ld_sys64(reinterpret_cast<const uint64_t*>(p))));
 }
 
 __device__ void dyn_mirror(const DynArgs& a) {
-  if (threadIdx.x != 0) return;
+  __shared__ uint32_t s_cmd[3];  // rows published, 0 running / 1 host close / 2 own close, close mode
+  const int tid = static_cast<int>(threadIdx.x);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t last = t0;
-  uint32_t mc = 0;
+  uint32_t mc = 0;  // rows mirrored so far
   for (;;) {
-    const uint32_t hc = dyn_ld_sys(&a.ctl->count);
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (dyn_ld_sys(&a.ctl->closed)) {
-      const uint32_t fc = dyn_ld_sys(&a.ctl->count);
-      const uint32_t mode = dyn_ld_sys(&a.ctl->mode);
-      for (int i = 0; i < kDynCopies; ++i) {
-        __hip_atomic_store(&a.mir[i].mode, mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.mir[i].count, fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.mir[i].closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      uint32_t hc = mc, st = 0, mode = OUT_ACC;
+      for (;;) {
+        const uint32_t c = dyn_ld_host(&a.ctl->count);
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (dyn_ld_host(&a.ctl->closed)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's table writes before its release
+          hc = dyn_ld_host(&a.ctl->count);
+          mode = dyn_ld_host(&a.ctl->mode);
+          st = 1;
+          break;
+        }
+        if (c > mc) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          hc = c;
+          last = now;
+          break;
+        }
+        if (now - last > a.idle_ticks || now - t0 > a.life_ticks) {
+          // nothing new for too long (or too long alive): the wave ends with the rows it has
+          st = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
       }
-      __hip_atomic_store(&a.ack->count, fc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.ack->state, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
+      s_cmd[0] = hc;
+      s_cmd[1] = st;
+      s_cmd[2] = mode;
     }
-    if (hc > mc) {
-      mc = hc;
-      last = now;
+    __syncthreads();
+    const uint32_t hc = s_cmd[0], st = s_cmd[1], mode = s_cmd[2];
+    // copy rows [mc, hc) of the host table, and at a final close the divisors and outputs
+    const int rows = static_cast<int>(hc - mc);
+    if (rows > 0) {
+      const int n = rows * a.num_segs;
+      for (int i = tid; i < n; i += static_cast<int>(blockDim.x)) {
+        const int t = i / rows;
+        const int64_t o = static_cast<int64_t>(t) * a.cap + mc + (i - t * rows);
+        dyn_st_sys64(a.ptab + o, dyn_ld_sys64(a.h_ptab + o));
+      }
+      for (int i = tid; i < rows; i += static_cast<int>(blockDim.x)) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(a.wtab) + mc + i;
+        dyn_st_sys64(d, dyn_ld_sys64(reinterpret_cast<const uint64_t*>(a.h_wtab) + mc + i));
+      }
+    }
+    if (st == 1 && mode != OUT_ACC) {
+      for (int t = tid; t < a.num_segs; t += static_cast<int>(blockDim.x)) {
+        dyn_st_sys64(reinterpret_cast<uint64_t*>(a.wtot) + t, dyn_ld_sys64(reinterpret_cast<const uint64_t*>(a.h_wtot) + t));
+        dyn_st_sys64(a.outs + t, dyn_ld_sys64(a.h_outs + t));
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();
+    if (tid == 0) {
+      const uint64_t w = dyn_word(hc, st != 0 ? 1u : 0u, st == 1 ? mode : static_cast<uint32_t>(OUT_ACC), a.epoch);
       for (int i = 0; i < kDynCopies; ++i)
-        __hip_atomic_store(&a.mir[i].count, mc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (now - last > a.idle_ticks || now - t0 > a.life_ticks) {
-      // nothing new for too long (or too long alive): the wave ends with the rows seen so far
-      for (int i = 0; i < kDynCopies; ++i) {
-        __hip_atomic_store(&a.mir[i].mode, static_cast<uint32_t>(OUT_ACC), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.mir[i].count, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.mir[i].closed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.mir[i].word, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st != 0) {
+        __hip_atomic_store(&a.ack->count, hc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ack->state, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      __hip_atomic_store(&a.ack->count, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.ack->state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
     }
-    __builtin_amdgcn_s_sleep(8);
+    if (st != 0) return;
+    mc = hc;
   }
 }
 
+// Geometry: the wave's fp64 accumulators stay in registers for the whole round, so as many
+// tiles as possible must be resident at once — a tile that is not waits for a resident one to
+// finish, i.e. for the close, and then folds every row after the arrivals instead of during them.
+// Two launches share the wave (one mirror, one protocol):
+//  * body tiles — every whole kDynTile-element tile of a segment: one-wave workgroups, kDynAE
+//    elements per lane (96: 192 VGPRs of accumulators, two 16-element load stages, <= 256 VGPRs
+//    = 2 waves per SIMD): 256 CUs x 4 SIMDs x 2 waves x 64 lanes x 96 = 12.6 M elements
+//    resident, e.g. all 1,883 body tiles of ResNet-18 (11.7 M parameters in 62 tensors);
+//  * edge tiles — what is left of each segment, in kDynEdgeTile-element tiles (kDynAEEdge per
+//    lane): whole 16-B vectors with clamped loads, the < 16 B past the last one by one lane with
+//    its accumulators in LDS (a tensor may end anywhere: nothing past its end is read).
+// Loads are double-buffered per 16 elements (8 for fp64 inputs), across client boundaries too.
+#ifndef FEDAVG_DYN_AE
+#define FEDAVG_DYN_AE 96
+#endif
+#ifndef FEDAVG_DYN_AE_EDGE
+#define FEDAVG_DYN_AE_EDGE 32
+#endif
+constexpr int kDynAE = FEDAVG_DYN_AE;
+constexpr int kDynAEEdge = FEDAVG_DYN_AE_EDGE;
+constexpr int kDynLanes = 64;
+constexpr int kDynTile = kDynAE * kDynLanes;
+constexpr int kDynEdgeTile = kDynAEEdge * kDynLanes;
 template <typename T>
-__global__ __launch_bounds__((Geo<T, 1, kTile1>::THREADS)) void dyn_wave_kernel(DynArgs a) {
-  if (blockIdx.x == 0) {
+using DynV = typename Vec16<T>::type;
+template <typename T, int AE>
+struct DynGeo {
+  using V = typename Vec16<T>::type;
+  static constexpr int N = Vec16<T>::n;  // elements per 16-B vector = per load stage
+  static constexpr int NV = AE / N;      // vectors (stages) per lane and client
+  // NB load buffers in a ring: NB - 1 vectors in flight while one is folded; NV % NB == 0 keeps
+  // every client's first stage on buffer 0, so the unrolled ring indices are compile-time
+  static constexpr int NB = NV % 8 == 0 ? 8 : NV % 6 == 0 ? 6 : NV % 4 == 0 ? 4 : 2;
+  static_assert(AE % N == 0 && NV % NB == 0, "lane slice in whole vectors, a whole number of rings");
+};
+
+// vector v of a client's tile slice into a ring buffer. PART (edge tiles): vectors at or past
+// `nfull` (the tile's whole vectors) re-read vector 0 instead; their fold adds zeros
+template <typename T, bool PART>
+__device__ __forceinline__ void dyn_issue(DynV<T>& b, gptr<const DynV<T>> base, int v, int li, int nfull) {
+  const int idx = v * kDynLanes + li;
+  b = __builtin_nontemporal_load(base + ((!PART || idx < nfull) ? idx : 0));
+}
+// fold vector v into the accumulators: acc = acc + round(x * w), in arrival order
+template <typename T, int AE, bool PART>
+__device__ __forceinline__ void dyn_fold_vec(double (&acc)[AE], const DynV<T>& b, int v, double w, int li, int nfull) {
+  constexpr int N = Vec16<T>::n;
+  double x[N];
+  expand<T>(b, x);
+  const bool in = !PART || v * kDynLanes + li < nfull;
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    double& r = acc[v * N + q];
+    r = fold<FOLD_MULADD>(r, in ? x[q] : 0.0, w, 0.0);
+  }
+}
+
+// one client's tile slice through the load ring: before vector v is folded, vector v + NB - 1 is
+// issued (past the slice's end: the next client's first vectors, when NEXT). The scheduling groups
+// pin that order — left alone, the scheduler hoists every load of the client to its top and runs
+// out of registers beside the accumulators.
+template <typename T, int AE, bool PART, bool NEXT, int NB>
+__device__ __forceinline__ void dyn_fold_client(double (&acc)[AE], DynV<T> (&buf)[NB], gptr<const DynV<T>> cur,
+                                                gptr<const DynV<T>> nxt, double w, int li, int nfull) {
+  constexpr int NV = AE / Vec16<T>::n;
+  static_assert(NV % NB == 0, "a whole number of rings per client");
+  constexpr int VALU_PER_VEC = Vec16<T>::n * (sizeof(T) == 8 ? 2 : sizeof(T) == 4 ? 3 : 4);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int ahead = v + NB - 1;
+    if (ahead < NV) {
+      dyn_issue<T, PART>(buf[ahead % NB], cur, ahead, li, nfull);
+    } else if (NEXT) {
+      dyn_issue<T, PART>(buf[ahead % NB], nxt, ahead - NV, li, nfull);
+    }
+    dyn_fold_vec<T, AE, PART>(acc, buf[v % NB], v, w, li, nfull);
+    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);             // VMEM_READ: the vector ahead
+    __builtin_amdgcn_sched_group_barrier(0x2, VALU_PER_VEC, 0);  // VALU: this vector's fold
+  }
+}
+// the ring's first NB - 1 vectors of a client
+template <typename T, bool PART, int NB>
+__device__ __forceinline__ void dyn_prime(DynV<T> (&buf)[NB], gptr<const DynV<T>> base, int li, int nfull) {
+#pragma unroll
+  for (int v = 0; v + 1 < NB; ++v) dyn_issue<T, PART>(buf[v], base, v, li, nfull);
+}
+
+// EDGE = false: the body tiles, workgroup 0 the mirror; EDGE = true: the edge tiles
+template <typename T, bool EDGE>
+__global__ __attribute__((amdgpu_flat_work_group_size(kDynLanes, kDynLanes), amdgpu_waves_per_eu(2, 8)))
+void dyn_wave_kernel(DynArgs a) {
+  if (!EDGE && blockIdx.x == 0) {
     dyn_mirror(a);
     return;
   }
-  constexpr int AE = Geo<T, 1, kTile1>::AE;
-  constexpr int LANES = Geo<T, 1, kTile1>::LANES;
-  constexpr int TILE = Geo<T, 1, kTile1>::TILE;
-  using LL = LaneLoader<T, LANES, true, true, AE>;
-  using LC = LaneLoader<T, LANES, false, true, AE>;
-  using V = typename LL::V;
-  constexpr int N = LL::N;
-  constexpr int VPL = LL::VPL;
-  constexpr int CU_LOADS = (FEDAVG_CU_BYTES / (VPL * 16)) < 2 ? 2 : (FEDAVG_CU_BYTES / (VPL * 16));
+  constexpr int AE = EDGE ? kDynAEEdge : kDynAE;
+  constexpr int TILE = EDGE ? kDynEdgeTile : kDynTile;
+  using G = DynGeo<T, AE>;
+  using V = typename G::V;
+  constexpr int N = G::N;
+  // the close works in groups of CE elements (CH vectors): one exact-division block each
+  constexpr int CE = sizeof(T) == 8 ? 8 : 16;
+  constexpr int CH = CE / N;
+  constexpr int NCH = AE / CE;
+  static_assert(AE % CE == 0, "whole division groups");
   __shared__ uint64_t sp[kDynBatch];
   __shared__ double sw[kDynBatch];
   __shared__ int32_t s_n;
@@ -977,56 +1126,72 @@ __global__ __launch_bounds__((Geo<T, 1, kTile1>::THREADS)) void dyn_wave_kernel(
   __shared__ double s_W;
   __shared__ uint64_t s_out;
 
-  const TileDesc td = load_tile(a.tiles, blockIdx.x - 1);
+  __shared__ double s_tail[N];
+
+  const TileDesc td = load_tile(EDGE ? a.edge_tiles : a.tiles, blockIdx.x - (EDGE ? 0 : 1));
   const int seg = td.seg;
   const int count = td.count;
-  const bool full = count == TILE;
+  const bool full = !EDGE;  // body tiles are whole (count == TILE)
+  const int nfull = count / N;        // whole 16-B vectors of the tile
+  const int tail = count - nfull * N; // elements past them (a segment's last tile)
   const int li = static_cast<int>(threadIdx.x);
+  if (li < N) s_tail[li] = -0.0;
   const int64_t elem_off = td.start * static_cast<int64_t>(sizeof(T));
   const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;  // SegDesc::acc_off
 
-  double acc[AE];
+  double acc[AE];  // element (v * 64 + li) * N + q of the tile at acc[v * N + q]
 #pragma unroll
   for (int i = 0; i < AE; ++i) acc[i] = -0.0;  // the additive identity (see tile_body)
+  (void)TILE;
 
-  DynMirror* const mir = a.mir + (blockIdx.x % kDynCopies);
+  const DynMirror* const mir = a.mir + (blockIdx.x % kDynCopies);
   int k = 0;             // rows folded
-  uint32_t avail = 0;    // rows known published (thread 0)
+  uint32_t avail = 0;    // rows known mirrored (thread 0)
+  uint32_t closed = 0;   // the mirror closed the wave (thread 0)
+  uint32_t cmode = OUT_ACC;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (threadIdx.x == 0) {
-      uint32_t closed = 0;
-      while (avail <= static_cast<uint32_t>(k) && !closed) {
-        const uint32_t c = dyn_ld_agent(&mir->count);
-        if (c > avail) {
-          avail = c;
-          break;
+      if (avail <= static_cast<uint32_t>(k) && !closed) {
+        for (;;) {  // relaxed polls of the mirror word
+          const uint64_t w = __hip_atomic_load(&mir->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (static_cast<uint32_t>(w >> 32) == a.epoch) {
+            const uint32_t c = static_cast<uint32_t>(w) & 0xffffffu;
+            if ((w >> 24) & 1u) {
+              closed = 1;
+              cmode = static_cast<uint32_t>(w >> 25) & 7u;
+              avail = c;
+              break;
+            }
+            if (c > avail) {
+              avail = c;
+              break;
+            }
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > a.life_ticks + 100000000ull) {  // life + 1 s
+            __hip_atomic_store(&a.ack->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            avail = static_cast<uint32_t>(k);
+            closed = 1;
+            cmode = OUT_ACC;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(32);
         }
-        if (dyn_ld_agent(&mir->closed)) {
-          avail = dyn_ld_agent(&mir->count);
-          closed = 1;
-          break;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > a.life_ticks + 100000000ull) {  // life + 1 s
-          __hip_atomic_store(&a.ack->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          avail = static_cast<uint32_t>(k);
-          closed = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(16);
+        // no acquire: every handed-off byte (the mirror's table) is stored and loaded with
+        // system-coherent accesses, which no L1 / L2 copy can serve stale (Guideline 16's sc1
+        // form); the client tensors were complete before their rows were published
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
       const int n = static_cast<int>(avail) - k;
       s_n = n < 0 ? 0 : (n > kDynBatch ? kDynBatch : n);
+      s_mode = static_cast<int>(cmode);
     }
     __syncthreads();
     const int n = __builtin_amdgcn_readfirstlane(s_n);
     if (n == 0) break;
-    if (li < n) {  // the batch's rows of this tile's segment, straight from the host table
-      sp[li] = __hip_atomic_load(a.ptab + static_cast<int64_t>(seg) * a.cap + k + li, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint64_t wb = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.wtab) + k + li, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_SYSTEM);
-      sw[li] = __longlong_as_double(static_cast<long long>(wb));
+    if (li < n) {  // the batch's rows of this tile's segment, from the mirror's device table
+      sp[li] = dyn_ld_sys64(a.ptab + static_cast<int64_t>(seg) * a.cap + k + li);
+      sw[li] = dyn_ld_sysf(a.wtab + k + li);
     }
     __syncthreads();
     auto client = [&](int i) -> gptr<const T> {
@@ -1035,123 +1200,101 @@ __global__ __launch_bounds__((Geo<T, 1, kTile1>::THREADS)) void dyn_wave_kernel(
       const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p >> 32));
       return to_global<T>(reinterpret_cast<const void*>(((static_cast<uint64_t>(hi) << 32) | lo) + elem_off));
     };
-    if (full) {
-      // groups of CU_LOADS clients, every load of a group issued before its fold (tile_body)
-      for (int g = 0; g < n; g += CU_LOADS) {
-        V buf[CU_LOADS][VPL];
-        double wk[CU_LOADS];
-#pragma unroll
-        for (int c = 0; c < CU_LOADS; ++c) {
-          const int kc = min(g + c, n - 1);  // a short last group re-loads its last client
-          wk[c] = sw[kc];
-          LL::load_raw(client(kc), li, buf[c]);
+    if (EDGE ? nfull > 0 : true) {  // the tile's whole vectors (all of a body tile's)
+      constexpr int NB = G::NB;
+      V buf[NB];
+      dyn_prime<T, EDGE, NB>(buf, (gptr<const V>)client(0), li, nfull);
+      int i = 0;
+      for (; i + 1 < n; ++i)
+        dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i + 1), sw[i], li,
+                                               nfull);
+      dyn_fold_client<T, AE, EDGE, false, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i), sw[i], li, nfull);
+    }
+    if constexpr (EDGE) {
+      if (tail > 0 && li == 0) {  // the < N elements past them, one lane, accumulators in LDS
+        for (int i = 0; i < n; ++i) {
+          const gptr<const T> base = client(i);
+          for (int q = 0; q < tail; ++q) s_tail[q] = fold<FOLD_MULADD>(s_tail[q], load_g<T>(base, nfull * N + q), sw[i], 0.0);
         }
-#pragma unroll
-        for (int c = 0; c < CU_LOADS; ++c) {
-          const bool use = g + c < n;
-#pragma unroll
-          for (int v = 0; v < VPL; ++v) {
-            double x[N];
-            expand<T>(buf[c][v], x);
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-              double& r = acc[v * N + j];
-              const double nv = fold<FOLD_MULADD>(r, x[j], wk[c], 0.0);
-              r = use ? nv : r;
-            }
-          }
-        }
-      }
-    } else {
-      for (int i = 0; i < n; ++i) {
-        const double wk = sw[i];
-        double x[AE];
-        LC::load_checked(client(i), li, count, x);
-#pragma unroll
-        for (int j = 0; j < AE; ++j) acc[j] = fold<FOLD_MULADD>(acc[j], x[j], wk, 0.0);
       }
     }
     k += n;
     __syncthreads();  // sp / sw are refilled by the next batch
   }
 
-  // the close: the mode, and for a final close the segment's divisor and output
-  if (threadIdx.x == 0) {
-    const int mode = static_cast<int>(dyn_ld_agent(&mir->mode));
-    s_mode = mode;
-    if (mode != OUT_ACC) {
-      s_W = __longlong_as_double(static_cast<long long>(__hip_atomic_load(
-          reinterpret_cast<const uint64_t*>(a.wtot) + seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
-      s_out = __hip_atomic_load(a.outs + seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  __syncthreads();
+  // the close: the mode (read with the closing word), and for a final close the segment's
+  // divisor and output from the mirror's device table
   const int mode = __builtin_amdgcn_readfirstlane(s_mode);
-  bool bad_acc = false;
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int e = (v * LANES + li) * N;
-#pragma unroll
-    for (int j = 0; j < N; ++j) bad_acc |= (full || e + j < count) && (acc[v * N + j] != acc[v * N + j]);
+  if (mode != OUT_ACC) {
+    if (threadIdx.x == 0) {
+      s_W = dyn_ld_sysf(a.wtot + seg);
+      s_out = dyn_ld_sys64(a.outs + seg);
+    }
+    __syncthreads();
   }
-  if (mode == OUT_ACC) {
-    if (k == 0) return;  // nothing folded: the accumulator holds nothing for this round
-    const gptr<double> ap = to_global_mut<double>(a.acc + acc_base);
+  // the close, a load stage's elements at a time: vector (c * CH + j) * 64 + li of the tile
+  // (a partial tile: its whole vectors here, its tail elements from LDS below)
+  bool bad_acc = false, bad_res = false;
+  const bool final_close = mode != OUT_ACC;
+  if (!final_close && k == 0) return;  // nothing folded: the accumulator holds nothing for this round
+  const double W = final_close ? s_W : 1.0;
+  void* const out_raw = final_close ? reinterpret_cast<void*>(s_out) : reinterpret_cast<void*>(a.acc + acc_base);
+  const int64_t out_off = final_close ? td.start : 0;
+  const bool f32_out = mode == OUT_F32;
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int e = (v * LANES + li) * N;
+  for (int c = 0; c < NCH; ++c) {
+    double res[CE];
+    bool in[CH];
 #pragma unroll
-      for (int j = 0; j < N; j += 2) {
-        if (full || e + j + 2 <= count) {
-          store_out((gptr<f64x2>)(ap + e + j), f64x2{acc[v * N + j], acc[v * N + j + 1]});
-        } else {
-          if (e + j < count) ap[e + j] = acc[v * N + j];
-          if (e + j + 1 < count) ap[e + j + 1] = acc[v * N + j + 1];
-        }
+    for (int j = 0; j < CH; ++j) in[j] = full || (c * CH + j) * kDynLanes + li < nfull;
+#pragma unroll
+    for (int i = 0; i < CE; ++i) bad_acc |= in[i / N] && acc[c * CE + i] != acc[c * CE + i];
+    if (final_close) {
+      exact_div_block<CE>(acc + c * CE, res, W);  // the fused divide (_apply_total_weight, :71-74)
+#pragma unroll
+      for (int i = 0; i < CE; ++i) bad_res |= in[i / N] && res[i] != res[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < CE; ++i) res[i] = acc[c * CE + i];
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (!in[j]) continue;
+      const int64_t e = out_off + static_cast<int64_t>((c * CH + j) * kDynLanes + li) * N;
+      const double* r = res + j * N;
+      if (f32_out) {
+        const gptr<float> op = to_global_mut<float>(out_raw) + e;
+#pragma unroll
+        for (int q = 0; q < N; q += 2)
+          store_out((gptr<f32x2>)(op + q), f32x2{static_cast<float>(r[q]), static_cast<float>(r[q + 1])});
+      } else {
+        const gptr<double> op = to_global_mut<double>(out_raw) + e;
+#pragma unroll
+        for (int q = 0; q < N; q += 2) store_out((gptr<f64x2>)(op + q), f64x2{r[q], r[q + 1]});
       }
     }
-    if (__ballot(bad_acc) != 0ull && (threadIdx.x & 63) == 0) raise_flag(a.flag, 0);
-    return;
+    __builtin_amdgcn_sched_group_barrier(0x40, CE / 2, 0);  // VMEM_WRITE: the stage's stores
   }
-  // final close: the fused divide (_apply_total_weight, :71-74) and the :93 / :97 checks
-  double res[AE];
-  exact_div_block<AE>(acc, res, s_W);
-  bool bad_res = false;
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int e = (v * LANES + li) * N;
-#pragma unroll
-    for (int j = 0; j < N; ++j) bad_res |= (full || e + j < count) && (res[v * N + j] != res[v * N + j]);
-  }
-  void* const out_raw = reinterpret_cast<void*>(s_out);
-  if (mode == OUT_F32) {
-    const gptr<float> op = to_global_mut<float>(out_raw) + td.start;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int e = (v * LANES + li) * N;
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-        if (full || e + j < count) op[e + j] = static_cast<float>(res[v * N + j]);
-    }
-  } else {
-    const gptr<double> op = to_global_mut<double>(out_raw) + td.start;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int e = (v * LANES + li) * N;
-#pragma unroll
-      for (int j = 0; j < N; j += 2) {
-        if (full || e + j + 2 <= count) {
-          store_out((gptr<f64x2>)(op + e + j), f64x2{res[v * N + j], res[v * N + j + 1]});
-        } else {
-          if (e + j < count) op[e + j] = res[v * N + j];
-          if (e + j + 1 < count) op[e + j + 1] = res[v * N + j + 1];
-        }
+  if (tail > 0 && li == 0) {  // a partial tile's last < N elements
+    for (int q = 0; q < tail; ++q) {
+      const double t = s_tail[q];
+      double r = t;
+      bad_acc |= t != t;
+      if (final_close) {
+        exact_div_block<1>(&t, &r, W);
+        bad_res |= r != r;
+      }
+      const int64_t e = out_off + static_cast<int64_t>(nfull) * N + q;
+      if (f32_out) {
+        to_global_mut<float>(out_raw)[e] = static_cast<float>(r);
+      } else {
+        to_global_mut<double>(out_raw)[e] = r;
       }
     }
   }
   const uint64_t ba = __ballot(bad_acc);
   const uint64_t br = __ballot(bad_res);
-  if ((ba | br) != 0ull && (threadIdx.x & 63) == 0) {
+  if ((ba | br) != 0ull && li == 0) {
     if (ba) raise_flag(a.flag, 0);
     if (br) raise_flag(a.flag, 1);
   }
@@ -2040,6 +2183,14 @@ struct fedavg_ctx {
     char* dev_alias = nullptr;
     size_t bytes = 0;
     char* mirror = nullptr;    // kDynCopies DynMirror (device)
+    char* dtab = nullptr;      // the device copy of the tables (DynLayout offsets, device memory)
+    std::vector<TileDesc> tiles;       // body tiles: the whole kDynTile-element tiles of each segment
+    std::vector<TileDesc> edge_tiles;  // edge tiles: the rest, in <= kDynEdgeTile-element tiles
+    TileDesc* d_tiles = nullptr;
+    TileDesc* d_edge_tiles = nullptr;
+    hipStream_t edge_stream = nullptr;  // the edge launch runs beside the body launch
+    hipEvent_t edge_done = nullptr;
+    uint32_t epoch = 0;        // waves opened on this context (tags the mirror word)
     hipStream_t stream = nullptr;
     hipEvent_t start = nullptr, done = nullptr;
     std::vector<double> wsum;  // per segment, the published rows' weights in arrival order
@@ -2962,9 +3113,15 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
     c->dyn.active = false;
   }
   if (c->dyn.stream) (void)hipStreamSynchronize(c->dyn.stream);
+  if (c->dyn.edge_stream) (void)hipStreamSynchronize(c->dyn.edge_stream);
   (void)hipDeviceSynchronize();
   if (c->dyn.host) (void)hipHostFree(c->dyn.host);
   if (c->dyn.mirror) (void)hipFree(c->dyn.mirror);
+  if (c->dyn.dtab) (void)hipFree(c->dyn.dtab);
+  if (c->dyn.d_tiles) (void)hipFree(c->dyn.d_tiles);
+  if (c->dyn.d_edge_tiles) (void)hipFree(c->dyn.d_edge_tiles);
+  if (c->dyn.edge_done) (void)hipEventDestroy(c->dyn.edge_done);
+  if (c->dyn.edge_stream) (void)hipStreamDestroy(c->dyn.edge_stream);
   if (c->dyn.start) (void)hipEventDestroy(c->dyn.start);
   if (c->dyn.done) (void)hipEventDestroy(c->dyn.done);
   if (c->dyn.stream) (void)hipStreamDestroy(c->dyn.stream);
@@ -3025,6 +3182,7 @@ int32_t fedavg_reset(fedavg_ctx* c, void* stream) {
   if (c->dyn.active) {  // an abandoned round's dynamic wave: ended and drained before the reset
     FEDAVG_RET(fedavg_dyn_close(c, nullptr, FEDAVG_F64, stream, nullptr, nullptr));
     FEDAVG_HIP_TRY(hipStreamSynchronize(c->dyn.stream));
+    FEDAVG_HIP_TRY(hipStreamSynchronize(c->dyn.edge_stream));
   }
   std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
@@ -3908,31 +4066,50 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   if (d.active) return fail(FEDAVG_ERR_STATE, "a dynamic wave is already open");
   if (in_dtype != FEDAVG_F32 && in_dtype != FEDAVG_F16 && in_dtype != FEDAVG_BF16 && in_dtype != FEDAVG_F64)
     return fail(FEDAVG_ERR_INVALID, "dynamic waves take fp32 / fp16 / bf16 / fp64 inputs");
-  if (max_clients < 1) return fail(FEDAVG_ERR_INVALID, "max_clients must be >= 1");
+  if (max_clients < 1 || max_clients >= (1 << 24)) return fail(FEDAVG_ERR_INVALID, "max_clients must be in [1, 2^24)");
   for (int t = 0; t < c->T; ++t)
     if (c->valid[t]) return fail(FEDAVG_ERR_STATE, "a dynamic wave opens a round: the accumulator already holds data");
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   if (!d.stream) {
     FEDAVG_HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    FEDAVG_HIP_TRY(hipStreamCreateWithFlags(&d.edge_stream, hipStreamNonBlocking));
+    FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.edge_done, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.start, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.mirror), sizeof(DynMirror) * kDynCopies));
+    FEDAVG_HIP_TRY(hipMemset(d.mirror, 0, sizeof(DynMirror) * kDynCopies));  // epoch 0: never a wave's
+    for (int t = 0; t < c->T; ++t) {  // body tiles, then each segment's rest as edge tiles
+      const int64_t n = c->seg_numel[t], body = n / kDynTile * kDynTile;
+      for (int64_t s0 = 0; s0 < body; s0 += kDynTile) d.tiles.push_back(TileDesc{t, kDynTile, s0});
+      for (int64_t s0 = body; s0 < n; s0 += kDynEdgeTile)
+        d.edge_tiles.push_back(TileDesc{t, static_cast<int32_t>(std::min<int64_t>(kDynEdgeTile, n - s0)), s0});
+    }
+    for (auto [host, dev] : {std::pair{&d.tiles, &d.d_tiles}, std::pair{&d.edge_tiles, &d.d_edge_tiles}}) {
+      if (host->empty()) continue;
+      FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(dev), sizeof(TileDesc) * host->size()));
+      FEDAVG_HIP_TRY(hipMemcpy(*dev, host->data(), sizeof(TileDesc) * host->size(), hipMemcpyHostToDevice));
+    }
     d.idle_ticks = dyn_env_us("FEDAVG_DYN_IDLE_US", 500) * 100;      // s_memrealtime: 100 MHz
     d.life_ticks = dyn_env_us("FEDAVG_DYN_LIFE_US", 2000000) * 100;
   }
   if (d.cap < max_clients) {
     FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));  // the previous wave has left the old block
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
     if (d.host) FEDAVG_HIP_TRY(hipHostFree(d.host));
+    if (d.dtab) FEDAVG_HIP_TRY(hipFree(d.dtab));
     d.host = nullptr;
+    d.dtab = nullptr;
     d.cap = 0;
     const int cap = std::max(max_clients, 64);
     const DynLayout L(c->T, cap);
     FEDAVG_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.host), L.bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.dtab), L.bytes));
     FEDAVG_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d.dev_alias), d.host, 0));
     d.cap = cap;
     d.bytes = L.bytes;
   }
   FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));  // the previous wave read its block to the end
+  FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
   const DynLayout L(c->T, d.cap);
   DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
   DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);
@@ -3945,33 +4122,56 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   d.wsum.assign(c->T, -0.0);
   d.published = 0;
   d.in_dtype = in_dtype;
-  // the wave starts behind the caller's stream (what it enqueued so far), on the private stream
+  // the wave starts behind the caller's stream (what it enqueued so far), on the private stream;
+  // an idle caller's stream (the usual case: the previous round ended on the host) needs no
+  // cross-stream dependency, which costs two queue packets and ~40 us before the launch starts
   hipStream_t s = static_cast<hipStream_t>(stream);
-  FEDAVG_HIP_TRY(hipEventRecord(d.start, s));
-  FEDAVG_HIP_TRY(hipStreamWaitEvent(d.stream, d.start, 0));
-  FEDAVG_HIP_TRY(hipMemsetAsync(d.mirror, 0, sizeof(DynMirror) * kDynCopies, d.stream));
+  if (hipStreamQuery(s) != hipSuccess) {
+    FEDAVG_HIP_TRY(hipEventRecord(d.start, s));
+    FEDAVG_HIP_TRY(hipStreamWaitEvent(d.stream, d.start, 0));
+    FEDAVG_HIP_TRY(hipStreamWaitEvent(d.edge_stream, d.start, 0));
+  }
+  d.epoch = d.epoch + 1 == 0 ? 1 : d.epoch + 1;
   DynArgs a{};
-  a.tiles = c->d_tiles1;
+  a.tiles = d.d_tiles;
+  a.edge_tiles = d.d_edge_tiles;
   a.segs = c->d_segs;
   a.acc = c->acc;
   a.flag = c->d_flag;
   a.ctl = reinterpret_cast<DynCtl*>(d.dev_alias + L.ctl);
   a.ack = reinterpret_cast<DynAck*>(d.dev_alias + L.ack);
-  a.wtot = reinterpret_cast<const double*>(d.dev_alias + L.wtot);
-  a.outs = reinterpret_cast<const uint64_t*>(d.dev_alias + L.outs);
-  a.wtab = reinterpret_cast<const double*>(d.dev_alias + L.wtab);
-  a.ptab = reinterpret_cast<const uint64_t*>(d.dev_alias + L.ptab);
+  a.h_wtot = reinterpret_cast<const double*>(d.dev_alias + L.wtot);
+  a.h_outs = reinterpret_cast<const uint64_t*>(d.dev_alias + L.outs);
+  a.h_wtab = reinterpret_cast<const double*>(d.dev_alias + L.wtab);
+  a.h_ptab = reinterpret_cast<const uint64_t*>(d.dev_alias + L.ptab);
+  a.wtot = reinterpret_cast<double*>(d.dtab + L.wtot);
+  a.outs = reinterpret_cast<uint64_t*>(d.dtab + L.outs);
+  a.wtab = reinterpret_cast<double*>(d.dtab + L.wtab);
+  a.ptab = reinterpret_cast<uint64_t*>(d.dtab + L.ptab);
   a.mir = reinterpret_cast<DynMirror*>(d.mirror);
-  a.num_tiles = static_cast<int32_t>(c->tiles1.size());
+  a.num_tiles = static_cast<int32_t>(d.tiles.size());
+  a.num_segs = c->T;
   a.cap = d.cap;
+  a.epoch = d.epoch;
   a.idle_ticks = d.idle_ticks;
   a.life_ticks = d.life_ticks;
-  const dim3 grid(static_cast<unsigned>(a.num_tiles + 1));
+  // the body launch (its workgroup 0 is the mirror) first, so its workgroups are resident first
+  const dim3 grid(static_cast<unsigned>(a.num_tiles + 1)), block(kDynLanes);
   switch (in_dtype) {
-    case FEDAVG_F32: hipLaunchKernelGGL(dyn_wave_kernel<float>, grid, dim3(Geo<float, 1, kTile1>::THREADS), 0, d.stream, a); break;
-    case FEDAVG_F16: hipLaunchKernelGGL(dyn_wave_kernel<__half>, grid, dim3(Geo<__half, 1, kTile1>::THREADS), 0, d.stream, a); break;
-    case FEDAVG_BF16: hipLaunchKernelGGL(dyn_wave_kernel<bf16_t>, grid, dim3(Geo<bf16_t, 1, kTile1>::THREADS), 0, d.stream, a); break;
-    default: hipLaunchKernelGGL(dyn_wave_kernel<double>, grid, dim3(Geo<double, 1, kTile1>::THREADS), 0, d.stream, a); break;
+    case FEDAVG_F32: hipLaunchKernelGGL((dyn_wave_kernel<float, false>), grid, block, 0, d.stream, a); break;
+    case FEDAVG_F16: hipLaunchKernelGGL((dyn_wave_kernel<__half, false>), grid, block, 0, d.stream, a); break;
+    case FEDAVG_BF16: hipLaunchKernelGGL((dyn_wave_kernel<bf16_t, false>), grid, block, 0, d.stream, a); break;
+    default: hipLaunchKernelGGL((dyn_wave_kernel<double, false>), grid, block, 0, d.stream, a); break;
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  if (!d.edge_tiles.empty()) {
+    const dim3 egrid(static_cast<unsigned>(d.edge_tiles.size()));
+    switch (in_dtype) {
+      case FEDAVG_F32: hipLaunchKernelGGL((dyn_wave_kernel<float, true>), egrid, block, 0, d.edge_stream, a); break;
+      case FEDAVG_F16: hipLaunchKernelGGL((dyn_wave_kernel<__half, true>), egrid, block, 0, d.edge_stream, a); break;
+      case FEDAVG_BF16: hipLaunchKernelGGL((dyn_wave_kernel<bf16_t, true>), egrid, block, 0, d.edge_stream, a); break;
+      default: hipLaunchKernelGGL((dyn_wave_kernel<double, true>), egrid, block, 0, d.edge_stream, a); break;
+    }
   }
   FEDAVG_HIP_TRY(hipGetLastError());
   d.active = true;
@@ -4051,9 +4251,14 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   FEDAVG_HIP_TRY(hipEventRecord(d.done, d.stream));
   FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.done, 0));
+  if (!d.edge_tiles.empty()) {
+    FEDAVG_HIP_TRY(hipEventRecord(d.edge_done, d.edge_stream));
+    FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.edge_done, 0));
+  }
   const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
   if (__atomic_load_n(&ack->error, __ATOMIC_ACQUIRE)) {
     FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
     std::fill(c->valid.begin(), c->valid.end(), 0);
     return fail(FEDAVG_ERR_HIP, "a dynamic wave's workgroup lost its mirror (the wave's results are invalid)");
   }

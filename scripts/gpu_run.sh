@@ -7,6 +7,7 @@
 #   bench                 the headline N=1 line (bench.py, default flags)
 #   alias<G>              the single-process peer round rehearsed with G aliased entries on cuda:0
 #   plugin / gradient     bench.py --workload plugin / gradient
+#   plugin_static / gradient_static   the same with the dynamic wave off (FEDAVG_DYN=0)
 #   pers_int / pers_float bench.py --workload personalized (integer / float weights)
 #   profile               scripts/profile.sh <out-tag> (kernel trace + FETCH/WRITE PMC passes)
 #   pers_pmc              scripts/gpu_pers_pmc.sh
@@ -43,6 +44,8 @@ for step in "$@"; do
             run alias$G 400 python -u bench.py --procs 1 --gpus "$G" --alias --no-probe --stage-timeout 200 ;;
     plugin) run plugin 300 python -u bench.py --workload plugin --no-cpu-baseline ;;
     gradient) run gradient 300 python -u bench.py --workload gradient --no-cpu-baseline ;;
+    plugin_static) FEDAVG_DYN=0 run plugin_static 300 python -u bench.py --workload plugin --no-cpu-baseline ;;
+    gradient_static) FEDAVG_DYN=0 run gradient_static 300 python -u bench.py --workload gradient --no-cpu-baseline ;;
     pers_int) run pers_int 300 python -u bench.py --workload personalized --pers-weights int --no-cpu-baseline --no-probe ;;
     pers_float) run pers_float 300 python -u bench.py --workload personalized --pers-weights float --no-cpu-baseline --no-probe ;;
     profile) run profile 900 bash scripts/profile.sh "$TAG" ;;

@@ -22,6 +22,13 @@ from tests.golden_io import bits_equal
 
 pytestmark = pytest.mark.gpu
 
+@pytest.fixture(autouse=True)
+def _patient_wave(monkeypatch):
+    # these rounds arrive slowly (each builds its tensors and the oracle's): a wave that may idle
+    # 1 s between publications folds them all (the idle test sets its own limit)
+    monkeypatch.setenv("FEDAVG_DYN_IDLE_US", "1000000")
+
+
 SHAPES = {"conv": (16, 3, 5, 5), "bias": (16,), "fc": (10, 700), "big": (3, 4096), "tail": (4096 + 37,)}
 
 
@@ -58,6 +65,9 @@ def test_plugin_rounds_bit_identical(hip_device, dtype, n, wave):
     algo = FedAVGAlgorithm(device=hip_device, wave_size=wave, dynamic_wave=True)
     for r in range(2):  # two rounds on one object: the wave reopens every round
         _round(algo, hip_device, n, 10 * n + r, dtype)
+    # every round's first wave folded by the dynamic wave; a single-wave round divided by it too
+    assert algo.dyn_stats["waves"] == 2 and algo.dyn_stats["rows"] == 2 * min(n, wave), algo.dyn_stats
+    assert algo.dyn_stats["finalized"] == (2 if n <= wave else 0), algo.dyn_stats
     algo.exit()
 
 
@@ -65,6 +75,7 @@ def test_plugin_rounds_bit_identical(hip_device, dtype, n, wave):
 def test_fractional_weights_and_result_dtypes(hip_device, result_dtype):
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True, result_dtype=result_dtype)
     _round(algo, hip_device, 11, 5, weights="float")
+    assert algo.dyn_stats == {"waves": 1, "rows": 11, "finalized": 1}
     algo.exit()
 
 
@@ -77,6 +88,7 @@ def test_a_row_it_cannot_take_closes_it_early(hip_device):
 
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
     _round(algo, hip_device, 9, 21, mutate=mutate)
+    assert algo.dyn_stats == {"waves": 1, "rows": 4, "finalized": 0}
     algo.exit()
 
 
@@ -94,19 +106,22 @@ def test_busy_stream_defers_publication(hip_device):
 
 
 def test_wave_ends_itself_when_arrivals_stop(hip_device, monkeypatch):
-    # FEDAVG_DYN_IDLE_US=200: a 30 ms gap between arrivals ends the wave with the rows it has;
+    # FEDAVG_DYN_IDLE_US=20000: a 200 ms gap between arrivals ends the wave with the rows it has;
     # the later rows go through the ordinary waves
-    monkeypatch.setenv("FEDAVG_DYN_IDLE_US", "200")
+    monkeypatch.setenv("FEDAVG_DYN_IDLE_US", "20000")
     monkeypatch.setenv("FEDAVG_DYN_BATCH", "1")
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
 
     def mutate(k, p):
         if k == 3:
             torch.cuda.synchronize()
-            time.sleep(0.03)
+            time.sleep(0.2)
         return p
 
     _round(algo, hip_device, 8, 23, mutate=mutate)
+    # (a publication the current stream defers joins the next arrival's: 1-3 rows before the gap)
+    st = algo.dyn_stats
+    assert st["waves"] == 1 and 1 <= st["rows"] <= 3 and st["finalized"] == 0, st
     algo.exit()
 
 
@@ -165,7 +180,7 @@ def test_c_abi_protocol(hip_device):
         assert ctx.dyn_state() == (True, 0)
         with pytest.raises(_native.NativeError):
             ctx.accumulate(table, torch.float32)  # refused while the wave is open
-        torch.cuda.synchronize(hip_device)
+        torch.cuda.current_stream(hip_device).synchronize()  # (a device-wide sync waits for the wave)
         assert ctx.dyn_publish(table) == 7
         folded, fin = ctx.dyn_close(outs, torch.float64)
         assert (folded, fin) == (7, True)
@@ -178,7 +193,7 @@ def test_c_abi_protocol(hip_device):
         for x, w in zip(dev[:4], ws[:4]):
             head.add_client([x], [w])
         ctx.dyn_open(torch.float32, 16)
-        torch.cuda.synchronize(hip_device)
+        torch.cuda.current_stream(hip_device).synchronize()  # (a device-wide sync waits for the wave)
         assert ctx.dyn_publish(head) == 4
         assert ctx.dyn_close(None) == (4, False)
         out.fill_(float("nan"))

@@ -1026,9 +1026,10 @@ def main_plugin(args: argparse.Namespace) -> int:
     # 83-93): the native-dtype gradient dict, in_round=True, the dataset size as weight
     in_round = args.workload == "gradient"
 
-    def messages() -> list:
-        return [ParameterMessage(parameter=dict(p), aggregation_weight=w, in_round=in_round)
-                for p, w in zip(params, weights)]
+    def messages():
+        # one message at a time, as the server receives them (each is handed over on arrival)
+        return (ParameterMessage(parameter=dict(p), aggregation_weight=w, in_round=in_round)
+                for p, w in zip(params, weights))
 
     host_s = [0.0]
 

@@ -160,6 +160,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__dyn_pub = 0                   # its rows published so far
         self.__dyn_closed: Any = None        # (table, rows folded) of the round's closed dynamic wave
         self.__dyn_round = False             # the round's first wave has been decided
+        # rounds of fewer updates than this (the previous round's count) skip the dynamic wave: its
+        # open / close cost more than the arrivals it hides (8-client gradient rounds)
+        self.dyn_min_rows = int(os.environ.get("FEDAVG_DYN_MIN_ROWS", 16))
+        self.__prev_arrivals: int | None = None  # the previous round's process_worker_data calls
+        self.__round_updates = 0
         # dynamic waves opened, rows they folded, waves that wrote the round's result themselves
         self.dyn_stats = {"waves": 0, "rows": 0, "finalized": 0}
         self.result_dtype = result_dtype
@@ -379,6 +384,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_id: int,
         worker_data: Message | None,
     ) -> bool:
+        self.__round_updates += 1
         if worker_data is not None and self._arrive_quick(worker_id, worker_data):
             return True
         res = super().process_worker_data(worker_id, worker_data)
@@ -931,7 +937,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     and self.device.type == "cuda"
                     and self.__multi_devices is None and self.accumulate and self.__default_hooks
                     and not self.wave_min and not self.eager_nan_check and self.__ew is False
-                    and not self.__table_delta and self.__table_dtype in _DYN_DTYPES):
+                    and not self.__table_delta and self.__table_dtype in _DYN_DTYPES
+                    and (self.__prev_arrivals is None or self.__prev_arrivals >= self.dyn_min_rows)):
                 return
             try:
                 self._context().dyn_open(self.__table_dtype, self.wave_size)
@@ -1036,6 +1043,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             except _native.NativeError:
                 pass
         self.__dyn_closed, self.__dyn_round = None, False
+        if self.__round_updates:
+            self.__prev_arrivals = self.__round_updates
+        self.__round_updates = 0
         self.__arrivals = 0
         self.__has_data = False
         self.__host_totals = {}

@@ -4108,8 +4108,10 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
     d.cap = cap;
     d.bytes = L.bytes;
   }
-  FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));  // the previous wave read its block to the end
-  FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
+  // the previous wave read its block to the end (its launches' completion events, recorded at its
+  // close; an event never recorded reads as complete)
+  if (hipEventQuery(d.done) != hipSuccess) FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
+  if (hipEventQuery(d.edge_done) != hipSuccess) FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
   const DynLayout L(c->T, d.cap);
   DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
   DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);

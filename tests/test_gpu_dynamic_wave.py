@@ -27,6 +27,7 @@ def _patient_wave(monkeypatch):
     # these rounds arrive slowly (each builds its tensors and the oracle's): a wave that may idle
     # 1 s between publications folds them all (the idle test sets its own limit)
     monkeypatch.setenv("FEDAVG_DYN_IDLE_US", "1000000")
+    monkeypatch.setenv("FEDAVG_DYN_MIN_ROWS", "0")  # every round opens one (the heuristic: its own test)
 
 
 SHAPES = {"conv": (16, 3, 5, 5), "bias": (16,), "fc": (10, 700), "big": (3, 4096), "tail": (4096 + 37,)}
@@ -68,6 +69,17 @@ def test_plugin_rounds_bit_identical(hip_device, dtype, n, wave):
     # every round's first wave folded by the dynamic wave; a single-wave round divided by it too
     assert algo.dyn_stats["waves"] == 2 and algo.dyn_stats["rows"] == 2 * min(n, wave), algo.dyn_stats
     assert algo.dyn_stats["finalized"] == (2 if n <= wave else 0), algo.dyn_stats
+    algo.exit()
+
+
+def test_small_rounds_skip_the_wave(hip_device, monkeypatch):
+    # FEDAVG_DYN_MIN_ROWS: after a round of fewer updates the next round folds in ordinary waves
+    monkeypatch.setenv("FEDAVG_DYN_MIN_ROWS", "16")
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    for r, n in enumerate((8, 8, 20, 20)):
+        _round(algo, hip_device, n, 40 + r)
+    # round 0 (no history) and round 3 (after a 20-update round) open a wave; rounds 1-2 do not
+    assert algo.dyn_stats == {"waves": 2, "rows": 28, "finalized": 2}, algo.dyn_stats
     algo.exit()
 
 

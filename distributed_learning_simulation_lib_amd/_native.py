@@ -150,7 +150,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     # dynamic waves (dyn_wave_kernel)
     "fedavg_dyn_open": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "fedavg_dyn_publish": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, POINTER(c_int32)]),
-    "fedavg_dyn_close": (c_int32, [c_void_p, _PP, c_int32, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    "fedavg_dyn_close": (c_int32, [c_void_p, _PP, c_int32, c_int32, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "fedavg_dyn_state": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     # single-process multi-device mode (multi_device.cpp)
     "fedavg_multi_create": (c_int32, [POINTER(c_void_p), POINTER(c_int32), c_int32, POINTER(c_int64), c_int32, _PP]),

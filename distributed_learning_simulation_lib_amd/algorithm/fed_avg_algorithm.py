@@ -959,12 +959,12 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         except _native.NativeError:
             self._dyn_close(None)
 
-    def _dyn_close(self, outs: Any, out_dtype: torch.dtype = torch.float64) -> bool:
+    def _dyn_close(self, outs: Any, out_dtype: torch.dtype = torch.float64, join: bool = True) -> bool:
         """Close the open dynamic wave: into ``outs`` (True: the round's result is written) or into
         the accumulator (the rows it folded; ``_dyn_rest`` gives the ordinary calls the rest)."""
         table = self.__dyn_table
         self.__dyn_table = None
-        folded, finalized = self._context().dyn_close(outs, out_dtype)
+        folded, finalized = self._context().dyn_close(outs, out_dtype, join)
         self.__dyn_closed = (table, folded)
         self.dyn_stats["rows"] += folded
         self.dyn_stats["finalized"] += int(finalized)
@@ -1102,7 +1102,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         done = False  # the dynamic wave wrote the result
         if table is not None and self.__dyn_table is table:
             self._dyn_publish()
-            done = self._dyn_close(None if (self.__ew or custom_divide or host_divide or delta) else outs, out_dtype)
+            # join=False: raise_on_nan below waits for the wave before anything reads the outputs
+            done = self._dyn_close(None if (self.__ew or custom_divide or host_divide or delta) else outs, out_dtype,
+                                   join=False)
         if not done and table is not None:
             table = self._dyn_rest(table)
         try:

@@ -2190,6 +2190,7 @@ struct fedavg_ctx {
     TileDesc* d_edge_tiles = nullptr;
     hipStream_t edge_stream = nullptr;  // the edge launch runs beside the body launch
     hipEvent_t edge_done = nullptr;
+    bool unjoined = false;  // a finalized wave closed with join = 0: fedavg_check waits for it
     uint32_t epoch = 0;        // waves opened on this context (tags the mirror word)
     hipStream_t stream = nullptr;
     hipEvent_t start = nullptr, done = nullptr;
@@ -2292,6 +2293,11 @@ void build_tiles(const std::vector<int64_t>& numel, int tile, std::vector<TileDe
     }
   }
 }
+
+// hipStreamQuery, asked twice: right after a synchronize, the first query of a stream that waited
+// on another stream's event (a dynamic wave's close) can still report the finished wait as
+// pending (ROCm 7.2, traced: each reset then enqueued a memset and the next open a dependency)
+bool stream_idle(hipStream_t s) { return hipStreamQuery(s) == hipSuccess || hipStreamQuery(s) == hipSuccess; }
 
 hipEvent_t take_event(fedavg_ctx* c) {
   if (!c->event_pool.empty()) {
@@ -3173,25 +3179,31 @@ int32_t fedavg_set_fused_fold(fedavg_ctx* c, int32_t enable) {
   return FEDAVG_OK;
 }
 
-int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, void* stream, int32_t* folded_out,
-                         int32_t* finalized_out);
+int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, int32_t join, void* stream,
+                         int32_t* folded_out, int32_t* finalized_out);
 
 int32_t fedavg_reset(fedavg_ctx* c, void* stream) {
   FEDAVG_RET(check_ctx(c));
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   if (c->dyn.active) {  // an abandoned round's dynamic wave: ended and drained before the reset
-    FEDAVG_RET(fedavg_dyn_close(c, nullptr, FEDAVG_F64, stream, nullptr, nullptr));
+    FEDAVG_RET(fedavg_dyn_close(c, nullptr, FEDAVG_F64, 1, stream, nullptr, nullptr));
     FEDAVG_HIP_TRY(hipStreamSynchronize(c->dyn.stream));
     FEDAVG_HIP_TRY(hipStreamSynchronize(c->dyn.edge_stream));
+  }
+  if (c->dyn.unjoined) {  // a finalized wave never checked: it may still raise a flag
+    FEDAVG_HIP_TRY(hipEventSynchronize(c->dyn.done));
+    FEDAVG_HIP_TRY(hipEventSynchronize(c->dyn.edge_done));
+    c->dyn.unjoined = false;
   }
   std::fill(c->wsum.begin(), c->wsum.end(), -0.0);
   std::fill(c->valid.begin(), c->valid.end(), 0);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipStreamQuery(s) == hipSuccess) {
+  if (stream_idle(s)) {
     // idle stream (the usual case: the previous round ended on the host): clear the host-coherent
     // flag words directly — an async memset is a blit kernel plus ~15 µs of queue latency per round
     for (int i = 0; i < 4; ++i) __atomic_store_n(&c->h_flag[i], 0u, __ATOMIC_RELEASE);
   } else {
+    if (const char* v = std::getenv("FEDAVG_DYN_TRACE"); v && *v == '1') std::fprintf(stderr, "[reset] busy stream: memset\n");
     FEDAVG_HIP_TRY(hipMemsetAsync(c->d_flag, 0, sizeof(uint32_t) * 4, s));
   }
   return FEDAVG_OK;
@@ -3424,6 +3436,11 @@ int32_t fedavg_check(fedavg_ctx* c, void* stream, uint32_t* flags_out) {
   FEDAVG_RET(check_ctx(c));
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (c->dyn.unjoined) {  // a finalized dynamic wave the caller's stream did not wait for
+    FEDAVG_HIP_TRY(hipEventSynchronize(c->dyn.done));
+    FEDAVG_HIP_TRY(hipEventSynchronize(c->dyn.edge_done));
+    c->dyn.unjoined = false;
+  }
   FEDAVG_HIP_TRY(hipStreamSynchronize(s));
   const uint32_t f = (__atomic_load_n(&c->h_flag[0], __ATOMIC_ACQUIRE) ? FEDAVG_FLAG_ACC_NAN : 0u) |
                      (__atomic_load_n(&c->h_flag[1], __ATOMIC_ACQUIRE) ? FEDAVG_FLAG_RESULT_NAN : 0u);
@@ -4034,6 +4051,32 @@ uint64_t dyn_env_us(const char* name, uint64_t dflt) {
   return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
 }
 
+// FEDAVG_DYN_TRACE=1: the host time of each step of fedavg_dyn_open / _close on stderr
+struct DynTrace {
+  bool on;
+  const char* what;
+  std::chrono::steady_clock::time_point t0, last;
+  char buf[256];
+  int len = 0;
+  explicit DynTrace(const char* w) : on(enabled()), what(w) { t0 = last = std::chrono::steady_clock::now(); }
+  static bool enabled() {
+    static const bool e = [] { const char* v = std::getenv("FEDAVG_DYN_TRACE"); return v && *v == '1'; }();
+    return e;
+  }
+  void mark(const char* step) {
+    if (!on || len > 200) return;
+    const auto now = std::chrono::steady_clock::now();
+    len += std::snprintf(buf + len, sizeof(buf) - len, " %s=%.1f", step,
+                         std::chrono::duration<double, std::micro>(now - last).count());
+    last = now;
+  }
+  ~DynTrace() {
+    if (on)
+      std::fprintf(stderr, "[dyn %s] total=%.1f us%s\n", what,
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(), buf);
+  }
+};
+
 int32_t dyn_wait_ack(fedavg_ctx* c, uint32_t* state, uint32_t* count) {
   const DynLayout L(c->T, c->dyn.cap);
   const DynAck* ack = reinterpret_cast<const DynAck*>(c->dyn.host + L.ack);
@@ -4069,6 +4112,7 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   if (max_clients < 1 || max_clients >= (1 << 24)) return fail(FEDAVG_ERR_INVALID, "max_clients must be in [1, 2^24)");
   for (int t = 0; t < c->T; ++t)
     if (c->valid[t]) return fail(FEDAVG_ERR_STATE, "a dynamic wave opens a round: the accumulator already holds data");
+  DynTrace tr("open");
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   if (!d.stream) {
     FEDAVG_HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
@@ -4110,8 +4154,10 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   }
   // the previous wave read its block to the end (its launches' completion events, recorded at its
   // close; an event never recorded reads as complete)
+  tr.mark("setup");
   if (hipEventQuery(d.done) != hipSuccess) FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
   if (hipEventQuery(d.edge_done) != hipSuccess) FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
+  tr.mark("prev");
   const DynLayout L(c->T, d.cap);
   DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
   DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);
@@ -4128,10 +4174,13 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   // an idle caller's stream (the usual case: the previous round ended on the host) needs no
   // cross-stream dependency, which costs two queue packets and ~40 us before the launch starts
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipStreamQuery(s) != hipSuccess) {
+  if (!stream_idle(s)) {
     FEDAVG_HIP_TRY(hipEventRecord(d.start, s));
     FEDAVG_HIP_TRY(hipStreamWaitEvent(d.stream, d.start, 0));
     FEDAVG_HIP_TRY(hipStreamWaitEvent(d.edge_stream, d.start, 0));
+    tr.mark("dep");
+  } else {
+    tr.mark("query");
   }
   d.epoch = d.epoch + 1 == 0 ? 1 : d.epoch + 1;
   DynArgs a{};
@@ -4166,6 +4215,7 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
     default: hipLaunchKernelGGL((dyn_wave_kernel<double, false>), grid, block, 0, d.stream, a); break;
   }
   FEDAVG_HIP_TRY(hipGetLastError());
+  tr.mark("body");
   if (!d.edge_tiles.empty()) {
     const dim3 egrid(static_cast<unsigned>(d.edge_tiles.size()));
     switch (in_dtype) {
@@ -4221,11 +4271,12 @@ int32_t fedavg_dyn_publish(fedavg_ctx* c, const void* const* client_ptrs, const 
   return FEDAVG_OK;
 }
 
-int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, void* stream, int32_t* folded_out,
-                         int32_t* finalized_out) {
+int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype, int32_t join, void* stream,
+                         int32_t* folded_out, int32_t* finalized_out) {
   FEDAVG_RET(check_ctx(c));
   auto& d = c->dyn;
   if (!d.active) return fail(FEDAVG_ERR_STATE, "no dynamic wave is open");
+  DynTrace tr("close");
   const int T = c->T;
   const DynLayout L(T, d.cap);
   DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
@@ -4248,15 +4299,21 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
   __atomic_store_n(&ctl->mode, mode, __ATOMIC_RELAXED);
   __atomic_store_n(&ctl->closed, 1u, __ATOMIC_RELEASE);
   uint32_t state = 0, folded = 0;
+  tr.mark("ctl");
   FEDAVG_RET(dyn_wait_ack(c, &state, &folded));
+  tr.mark("ack");
   d.active = false;
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  // an accumulator close always joins `stream` (the ordinary calls continue from the accumulator)
+  const bool joined = join || !(state == 1 && mode != OUT_ACC);
   FEDAVG_HIP_TRY(hipEventRecord(d.done, d.stream));
-  FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.done, 0));
+  if (joined) FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.done, 0));
   if (!d.edge_tiles.empty()) {
     FEDAVG_HIP_TRY(hipEventRecord(d.edge_done, d.edge_stream));
-    FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.edge_done, 0));
+    if (joined) FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.edge_done, 0));
   }
+  d.unjoined = !joined;
+  tr.mark("events");
   const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
   if (__atomic_load_n(&ack->error, __ATOMIC_ACQUIRE)) {
     FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));

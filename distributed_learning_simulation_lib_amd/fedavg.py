@@ -666,13 +666,14 @@ class FedAvgContext:
         return int(n.value)
 
     def dyn_close(self, outs: Sequence[torch.Tensor] | OutputTable | None = None,
-                  out_dtype: torch.dtype = torch.float64) -> tuple[int, bool]:
+                  out_dtype: torch.dtype = torch.float64, join: bool = True) -> tuple[int, bool]:
         """(rows folded, finalized): with ``outs`` the wave divides into them (finalized), else —
-        or when it ended itself — it leaves rows [0, folded) in the accumulator."""
+        or when it ended itself — it leaves rows [0, folded) in the accumulator. ``join=False``:
+        a finalized wave's outputs are complete after the next ``flags`` / ``raise_on_nan``."""
         ot = self._out_table(outs, out_dtype) if outs is not None else None
         folded, fin = ctypes.c_int32(), ctypes.c_int32()
-        _native.check(self._lib.fedavg_dyn_close(self._h, ot, out_code(out_dtype), self.stream, ctypes.byref(folded),
-                                                 ctypes.byref(fin)))
+        _native.check(self._lib.fedavg_dyn_close(self._h, ot, out_code(out_dtype), 1 if join else 0, self.stream,
+                                                 ctypes.byref(folded), ctypes.byref(fin)))
         return int(folded.value), bool(fin.value)
 
     def dyn_state(self) -> tuple[bool, int]:

@@ -463,13 +463,17 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
  *       aligned, one weight per row (else FEDAVG_ERR_INVALID: close the wave and fold the rest
  *       the ordinary way). Nothing is published (published = 0) while `stream` has unfinished
  *       work — the tensors of those rows may not be written yet.
- *   fedavg_dyn_close(ctx, out_ptrs or NULL, out_dtype, stream, &folded, &finalized)
+ *   fedavg_dyn_close(ctx, out_ptrs or NULL, out_dtype, join, stream, &folded, &finalized)
  *       fix the count. With out_ptrs (16-B aligned) the wave divides by the published rows'
  *       totals (arrival order) into the outputs: finalized = 1, the round is done (check with
  *       fedavg_check on `stream`). Otherwise — NULL outputs, or the wave ended itself after
  *       FEDAVG_DYN_IDLE_US (500) µs without a new row or FEDAVG_DYN_LIFE_US (2 s) in all — it
  *       stores the fp64 accumulator of rows [0, folded) (the context's state says so) and the
- *       caller folds rows [folded, K) with the ordinary calls. `stream` continues after the wave.
+ *       caller folds rows [folded, K) with the ordinary calls; `stream` then continues after the
+ *       wave. A finalized wave with join = 1 likewise orders `stream` after it; with join = 0
+ *       it does not — the outputs are complete once the next fedavg_check on this context
+ *       returns (it waits for the wave), which spares `stream` the cross-stream wait (a stream
+ *       that waited on another's event can still read as busy right after its synchronize).
  *   fedavg_dyn_state(ctx, &active, &published)
  * Per element the fold is the reference's arrival-order chain (separately rounded product and
  * sum): the bits equal fedavg_aggregate's.
@@ -477,8 +481,8 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
 int32_t fedavg_dyn_open(fedavg_ctx* ctx, int32_t in_dtype, int32_t max_clients, void* stream);
 int32_t fedavg_dyn_publish(fedavg_ctx* ctx, const void* const* client_ptrs, const double* weights, int32_t num_clients,
                            void* stream, int32_t* published_out);
-int32_t fedavg_dyn_close(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dtype, void* stream, int32_t* folded_out,
-                         int32_t* finalized_out);
+int32_t fedavg_dyn_close(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dtype, int32_t join, void* stream,
+                         int32_t* folded_out, int32_t* finalized_out);
 int32_t fedavg_dyn_state(const fedavg_ctx* ctx, int32_t* active, int32_t* published);
 
 /* =====================================================================================

@@ -213,5 +213,15 @@ def test_c_abi_protocol(hip_device):
         ctx.raise_on_nan()
         assert bits_equal(out.cpu().numpy(), want)
         ctx.reset()
+        # join=False: the caller's stream does not wait; the outputs are complete after the check
+        ctx.dyn_open(torch.float32, 16)
+        torch.cuda.current_stream(hip_device).synchronize()
+        assert ctx.dyn_publish(table) == 7
+        out.fill_(float("nan"))
+        torch.cuda.current_stream(hip_device).synchronize()
+        assert ctx.dyn_close(outs, torch.float64, join=False) == (7, True)
+        ctx.raise_on_nan()
+        assert bits_equal(out.cpu().numpy(), want)
+        ctx.reset()
     finally:
         ctx.close()

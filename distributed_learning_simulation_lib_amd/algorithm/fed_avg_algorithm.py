@@ -161,8 +161,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__dyn_closed: Any = None        # (table, rows folded) of the round's closed dynamic wave
         self.__dyn_round = False             # the round's first wave has been decided
         # rounds of fewer updates than this (the previous round's count) skip the dynamic wave: its
-        # open / close cost more than the arrivals it hides (8-client gradient rounds)
-        self.dyn_min_rows = int(os.environ.get("FEDAVG_DYN_MIN_ROWS", 16))
+        # open / close cost more than the arrivals it hides
+        self.dyn_min_rows = int(os.environ.get("FEDAVG_DYN_MIN_ROWS", 4))
         self.__prev_arrivals: int | None = None  # the previous round's process_worker_data calls
         self.__round_updates = 0
         # dynamic waves opened, rows they folded, waves that wrote the round's result themselves
@@ -948,15 +948,16 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self.dyn_stats["waves"] += 1
         elif self.__dyn_table is not table:
             return
-        if table.num_clients - self.__dyn_pub >= self.__dyn_batch:
-            self._dyn_publish()
+        if table.num_clients - self.__dyn_pub >= self.__dyn_batch or self.__dyn_pub == 0:
+            self._dyn_publish()  # (the first row at once: the wave starts folding)
 
     def _dyn_publish(self) -> None:
         """Every staged row of the dynamic wave's table to the wave (none while the current stream
         has unfinished work); a row it cannot take closes it with the rows it has."""
         try:
             self.__dyn_pub += self._context().dyn_publish(self.__dyn_table)
-        except _native.NativeError:
+        except _native.NativeError as e:
+            self.__dyn_pub += getattr(e, "published", 0)
             self._dyn_close(None)
 
     def _dyn_close(self, outs: Any, out_dtype: torch.dtype = torch.float64, join: bool = True) -> bool:

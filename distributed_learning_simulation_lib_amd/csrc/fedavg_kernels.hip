@@ -877,17 +877,17 @@ __global__ __launch_bounds__((Geo<T, SPLIT, TILEN>::THREADS)) void fedavg_tile_k
 // drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which ONE lane
 // publishes the count word (8-B agent-scope store); a tile workgroup polls that word relaxed and
 // needs no acquire (it reads no handed-off byte through L1 / L2). All stores are vector stores.
-struct DynCtl {     // host-coherent, written by the host
-  uint32_t count;   // rows published (release)
-  uint32_t closed;  // 1: `count` is final
-  uint32_t mode;    // at close: OUT_ACC / OUT_F32 / OUT_F64
-  uint32_t pad;
+struct DynCtl {     // host-coherent, written by the host: ONE 8-B word, so a poll is one PCIe read
+  uint64_t word;    // dyn_word(rows published, closed: the count is final, close mode, 0), release
+  uint64_t pad[7];
 };
 struct DynAck {     // host-coherent, written by the mirror workgroup
-  uint32_t state;   // 0 running, 1 closed by the host, 2 closed by the kernel (idle / lifetime)
-  uint32_t count;   // rows the wave folds
+  uint64_t word;    // state (0 running, 1 closed by the host, 2 closed by the kernel: idle /
+                    // lifetime) | rows the wave folds << 32 — one 8-B store
   uint32_t error;   // 1: a tile workgroup gave up waiting for the mirror
-  uint32_t pad;
+  uint32_t polls;   // the mirror's polls of the host word (FEDAVG_DYN_TRACE)
+  uint64_t t_seen;  // s_memrealtime when the mirror saw the close, and when it acknowledged it
+  uint64_t t_done;
 };
 struct DynMirror {  // device memory, written by the mirror workgroup: one copy per XCD (kDynCopies,
   uint64_t word;    // a cache line apart), so the tile workgroups' polls spread over 8 lines
@@ -927,9 +927,6 @@ struct DynArgs {
 
 constexpr int kDynBatch = 64;  // rows a tile workgroup fetches per poll (one per lane of wave 0)
 
-__device__ __forceinline__ uint32_t dyn_ld_host(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ uint64_t dyn_ld_sys64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -944,23 +941,28 @@ __device__ void dyn_mirror(const DynArgs& a) {
   __shared__ uint32_t s_cmd[3];  // rows published, 0 running / 1 host close / 2 own close, close mode
   const int tid = static_cast<int>(threadIdx.x);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t last = t0;
-  uint32_t mc = 0;  // rows mirrored so far
+  uint64_t last = t0, t_seen = 0;
+  uint32_t mc = 0, polls = 0;  // rows mirrored so far, host polls
   for (;;) {
     if (tid == 0) {
       uint32_t hc = mc, st = 0, mode = OUT_ACC;
       for (;;) {
-        const uint32_t c = dyn_ld_host(&a.ctl->count);
+        const uint64_t cw = dyn_ld_sys64(&a.ctl->word);
+        const uint32_t c = static_cast<uint32_t>(cw) & 0xffffffu;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (dyn_ld_host(&a.ctl->closed)) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's table writes before its release
-          hc = dyn_ld_host(&a.ctl->count);
-          mode = dyn_ld_host(&a.ctl->mode);
+        ++polls;
+        if ((cw >> 24) & 1u) {
+          // no fence: the host wrote the table before releasing the word, and every read of the
+          // host block is system-coherent (uncached), issued after this poll returned
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          hc = c;
+          mode = static_cast<uint32_t>(cw >> 25) & 7u;
           st = 1;
+          t_seen = now;
           break;
         }
         if (c > mc) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           hc = c;
           last = now;
           break;
@@ -982,7 +984,8 @@ __device__ void dyn_mirror(const DynArgs& a) {
     const int rows = static_cast<int>(hc - mc);
     if (rows > 0) {
       const int n = rows * a.num_segs;
-      for (int i = tid; i < n; i += static_cast<int>(blockDim.x)) {
+#pragma unroll 4
+      for (int i = tid; i < n; i += static_cast<int>(blockDim.x)) {  // (4 PCIe reads in flight)
         const int t = i / rows;
         const int64_t o = static_cast<int64_t>(t) * a.cap + mc + (i - t * rows);
         dyn_st_sys64(a.ptab + o, dyn_ld_sys64(a.h_ptab + o));
@@ -1005,8 +1008,11 @@ __device__ void dyn_mirror(const DynArgs& a) {
       for (int i = 0; i < kDynCopies; ++i)
         __hip_atomic_store(&a.mir[i].word, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (st != 0) {
-        __hip_atomic_store(&a.ack->count, hc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.ack->state, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ack->polls, polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ack->t_seen, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ack->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ack->word, static_cast<uint64_t>(st) | (static_cast<uint64_t>(hc) << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     if (st != 0) return;
@@ -3114,8 +3120,7 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
     // an open dynamic wave ends with the rows it has (its ACK arrives within a mirror poll)
     const DynLayout L(c->T, c->dyn.cap);
     DynCtl* ctl = reinterpret_cast<DynCtl*>(c->dyn.host + L.ctl);
-    __atomic_store_n(&ctl->mode, static_cast<uint32_t>(OUT_ACC), __ATOMIC_RELAXED);
-    __atomic_store_n(&ctl->closed, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(c->dyn.published), 1u, OUT_ACC, 0u), __ATOMIC_RELEASE);
     c->dyn.active = false;
   }
   if (c->dyn.stream) (void)hipStreamSynchronize(c->dyn.stream);
@@ -4085,10 +4090,11 @@ int32_t dyn_wait_ack(fedavg_ctx* c, uint32_t* state, uint32_t* count) {
   const auto t0 = std::chrono::steady_clock::now();
   const double limit_s = static_cast<double>(c->dyn.life_ticks) / 1e8 + 5.0;
   for (;;) {
-    const uint32_t st = __atomic_load_n(&ack->state, __ATOMIC_ACQUIRE);
+    const uint64_t aw = __atomic_load_n(&ack->word, __ATOMIC_ACQUIRE);
+    const uint32_t st = static_cast<uint32_t>(aw);
     if (st != 0) {
       *state = st;
-      *count = __atomic_load_n(&ack->count, __ATOMIC_ACQUIRE);
+      *count = static_cast<uint32_t>(aw >> 32);
       return FEDAVG_OK;
     }
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
@@ -4161,11 +4167,8 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   const DynLayout L(c->T, d.cap);
   DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
   DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);
-  __atomic_store_n(&ctl->count, 0u, __ATOMIC_RELAXED);
-  __atomic_store_n(&ctl->closed, 0u, __ATOMIC_RELAXED);
-  __atomic_store_n(&ctl->mode, static_cast<uint32_t>(OUT_ACC), __ATOMIC_RELAXED);
-  __atomic_store_n(&ack->state, 0u, __ATOMIC_RELAXED);
-  __atomic_store_n(&ack->count, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&ctl->word, dyn_word(0u, 0u, OUT_ACC, 0u), __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->word, uint64_t{0}, __ATOMIC_RELAXED);
   __atomic_store_n(&ack->error, 0u, __ATOMIC_RELEASE);
   d.wsum.assign(c->T, -0.0);
   d.published = 0;
@@ -4239,35 +4242,44 @@ int32_t fedavg_dyn_publish(fedavg_ctx* c, const void* const* client_ptrs, const 
   if (K < d.published || K > d.cap) return fail(FEDAVG_ERR_INVALID, "row count outside the wave's table");
   if (K == d.published) return FEDAVG_OK;
   const int T = c->T;
-  // rows the wave can take: every tensor present, 16-B aligned, one weight per row
-  for (int k = d.published; k < K; ++k) {
+  // rows the wave can take: every tensor present, 16-B aligned, one weight per row; the rows
+  // before the first one it cannot take are still published, then FEDAVG_ERR_INVALID
+  int good = K;
+  for (int k = d.published; k < K && good == K; ++k) {
     const double w = weights[static_cast<int64_t>(k) * T];
     for (int t = 0; t < T; ++t) {
       const void* p = client_ptrs[static_cast<int64_t>(k) * T + t];
       const double wt = weights[static_cast<int64_t>(k) * T + t];
-      if (!p || reinterpret_cast<uintptr_t>(p) % 16 != 0 || std::memcmp(&wt, &w, sizeof(double)) != 0)
-        return fail(FEDAVG_ERR_INVALID, "a row the dynamic wave cannot take (absent / unaligned tensor, per-tensor weights)");
+      if (!p || reinterpret_cast<uintptr_t>(p) % 16 != 0 || std::memcmp(&wt, &w, sizeof(double)) != 0) {
+        good = k;
+        break;
+      }
     }
   }
   // the caller's stream must have finished what it enqueued: the arrivals' tensors are then
   // complete (the wave runs on its own stream); otherwise nothing is published now
-  if (hipStreamQuery(static_cast<hipStream_t>(stream)) != hipSuccess) return FEDAVG_OK;
-  const DynLayout L(T, d.cap);
-  uint64_t* ptab = reinterpret_cast<uint64_t*>(d.host + L.ptab);
-  double* wtab = reinterpret_cast<double*>(d.host + L.wtab);
-  for (int k = d.published; k < K; ++k) {
-    const double w = weights[static_cast<int64_t>(k) * T];
-    wtab[k] = w;
-    for (int t = 0; t < T; ++t) {
-      ptab[static_cast<int64_t>(t) * d.cap + k] =
-          reinterpret_cast<uint64_t>(client_ptrs[static_cast<int64_t>(k) * T + t]);
-      d.wsum[t] += w;  // fed_avg_algorithm.py:59-62, arrival order
+  if (good > d.published && hipStreamQuery(static_cast<hipStream_t>(stream)) == hipSuccess) {
+    const DynLayout L(T, d.cap);
+    uint64_t* ptab = reinterpret_cast<uint64_t*>(d.host + L.ptab);
+    double* wtab = reinterpret_cast<double*>(d.host + L.wtab);
+    for (int k = d.published; k < good; ++k) {
+      const double w = weights[static_cast<int64_t>(k) * T];
+      wtab[k] = w;
+      for (int t = 0; t < T; ++t) {
+        ptab[static_cast<int64_t>(t) * d.cap + k] =
+            reinterpret_cast<uint64_t>(client_ptrs[static_cast<int64_t>(k) * T + t]);
+        d.wsum[t] += w;  // fed_avg_algorithm.py:59-62, arrival order
+      }
     }
+    DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
+    __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(good), 0u, OUT_ACC, 0u), __ATOMIC_RELEASE);
+    if (published_out) *published_out = good - d.published;
+    d.published = good;
+  } else if (good == K) {
+    return FEDAVG_OK;  // nothing published now (the stream is busy)
   }
-  DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
-  __atomic_store_n(&ctl->count, static_cast<uint32_t>(K), __ATOMIC_RELEASE);
-  if (published_out) *published_out = K - d.published;
-  d.published = K;
+  if (good < K)
+    return fail(FEDAVG_ERR_INVALID, "a row the dynamic wave cannot take (absent / unaligned tensor, per-tensor weights)");
   return FEDAVG_OK;
 }
 
@@ -4296,8 +4308,7 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
       mode = static_cast<uint32_t>(ok);
     }
   }
-  __atomic_store_n(&ctl->mode, mode, __ATOMIC_RELAXED);
-  __atomic_store_n(&ctl->closed, 1u, __ATOMIC_RELEASE);
+  __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(d.published), 1u, mode, 0u), __ATOMIC_RELEASE);
   uint32_t state = 0, folded = 0;
   tr.mark("ctl");
   FEDAVG_RET(dyn_wait_ack(c, &state, &folded));
@@ -4314,6 +4325,11 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
   }
   d.unjoined = !joined;
   tr.mark("events");
+  if (tr.on) {
+    const DynAck* ak = reinterpret_cast<const DynAck*>(d.host + L.ack);
+    tr.len += std::snprintf(tr.buf + tr.len, sizeof(tr.buf) - tr.len, " gpu_seen_to_ack=%.1f polls=%u",
+                            static_cast<double>(ak->t_done - ak->t_seen) / 100.0, ak->polls);
+  }
   const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
   if (__atomic_load_n(&ack->error, __ATOMIC_ACQUIRE)) {
     FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));

@@ -659,10 +659,15 @@ class FedAvgContext:
 
     def dyn_publish(self, table: ClientTable) -> int:
         """Hand the table's unpublished rows to the open wave; the rows published now (0 while
-        the current stream still has unfinished work). NativeError for rows the wave cannot take."""
+        the current stream still has unfinished work). NativeError for a row the wave cannot take
+        (its ``published``: the rows before it, published)."""
         p, w = _table_args(table)
         n = ctypes.c_int32()
-        _native.check(self._lib.fedavg_dyn_publish(self._h, p, w, table.num_clients, self.stream, ctypes.byref(n)))
+        st = self._lib.fedavg_dyn_publish(self._h, p, w, table.num_clients, self.stream, ctypes.byref(n))
+        if st != _native.OK:  # the rows before the one it cannot take were published: e.published
+            err = _native.NativeError(st, _native.last_error())
+            err.published = int(n.value)
+            raise err
         return int(n.value)
 
     def dyn_close(self, outs: Sequence[torch.Tensor] | OutputTable | None = None,

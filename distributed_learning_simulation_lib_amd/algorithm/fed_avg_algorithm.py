@@ -990,7 +990,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__table, self.__table_dtype = None, None
         if self.__dyn_table is table:  # a full dynamic wave: its rows stay in the accumulator
             self._dyn_publish()
-            self._dyn_close(None)
+            if self.__dyn_table is table:
+                self._dyn_close(None)
         table = self._dyn_rest(table)
         if table is None:
             return
@@ -1102,7 +1103,14 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         delta = self.__table_delta and table is not None
         done = False  # the dynamic wave wrote the result
         if table is not None and self.__dyn_table is table:
-            self._dyn_publish()
+            if self.__dyn_pub < table.num_clients and not torch.cuda.current_stream(self.device).query():
+                # the last arrivals' copies / conversions are still running: wait for them, as
+                # the one-launch path would, so the wave can take every row
+                torch.cuda.current_stream(self.device).synchronize()
+            self._dyn_publish()  # (a row it cannot take closes the wave here: the rest below)
+        if table is not None and self.__dyn_table is table and self.__dyn_pub < table.num_clients:
+            self._dyn_close(None)  # rows left unpublished: the wave keeps its rows, the rest below
+        if table is not None and self.__dyn_table is table:
             # join=False: raise_on_nan below waits for the wave before anything reads the outputs
             done = self._dyn_close(None if (self.__ew or custom_divide or host_divide or delta) else outs, out_dtype,
                                    join=False)

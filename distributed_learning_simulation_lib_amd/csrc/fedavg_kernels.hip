@@ -4056,6 +4056,10 @@ uint64_t dyn_env_us(const char* name, uint64_t dflt) {
   return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
 }
 
+// wave epochs, unique in the process: a mirror word left in recycled device memory by another
+// context's wave never matches a live one
+std::atomic<uint32_t> g_dyn_epoch{0};
+
 // FEDAVG_DYN_TRACE=1: the host time of each step of fedavg_dyn_open / _close on stderr
 struct DynTrace {
   bool on;
@@ -4127,7 +4131,11 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.start, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.mirror), sizeof(DynMirror) * kDynCopies));
-    FEDAVG_HIP_TRY(hipMemset(d.mirror, 0, sizeof(DynMirror) * kDynCopies));  // epoch 0: never a wave's
+    // epoch 0 is never a wave's; on the wave's own stream and waited for: a plain hipMemset
+    // is not ordered before a launch on a non-blocking stream, and a recycled allocation may
+    // hold another context's mirror words (epochs are process-wide besides: g_dyn_epoch)
+    FEDAVG_HIP_TRY(hipMemsetAsync(d.mirror, 0, sizeof(DynMirror) * kDynCopies, d.stream));
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
     for (int t = 0; t < c->T; ++t) {  // body tiles, then each segment's rest as edge tiles
       const int64_t n = c->seg_numel[t], body = n / kDynTile * kDynTile;
       for (int64_t s0 = 0; s0 < body; s0 += kDynTile) d.tiles.push_back(TileDesc{t, kDynTile, s0});
@@ -4185,7 +4193,8 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   } else {
     tr.mark("query");
   }
-  d.epoch = d.epoch + 1 == 0 ? 1 : d.epoch + 1;
+  d.epoch = g_dyn_epoch.fetch_add(1) + 1;
+  if (d.epoch == 0) d.epoch = g_dyn_epoch.fetch_add(1) + 1;
   DynArgs a{};
   a.tiles = d.d_tiles;
   a.edge_tiles = d.d_edge_tiles;

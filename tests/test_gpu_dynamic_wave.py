@@ -225,3 +225,32 @@ def test_c_abi_protocol(hip_device):
         ctx.reset()
     finally:
         ctx.close()
+
+
+def test_fresh_contexts_back_to_back(hip_device):
+    # each algorithm object has its own context and wave: a mirror allocation recycled from the
+    # previous context (same size) must not leak that context's words into the new wave
+    for r in range(6):
+        algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True, wave_size=64)
+        _round(algo, hip_device, 3 + r % 3, 70 + r)
+        assert algo.dyn_stats["waves"] == 1
+        algo.exit()
+
+
+def test_last_rows_still_being_copied(hip_device):
+    # host updates: every arrival leaves its copy on the stream; the final publication waits for
+    # the stream instead of dividing by the rows published so far (a mixed-dtype golden case
+    # once returned client 0 alone)
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    g = torch.Generator().manual_seed(9)
+    oracle = OracleFedAvg()
+    for k in range(6):
+        p = {name: torch.randn(s, generator=g) for name, s in SHAPES.items()}
+        w = 100 + 17 * k
+        algo.process_worker_data(k, ParameterMessage(parameter=dict(p), aggregation_weight=w))  # host tensors
+        oracle.process_worker_data(k, OracleMessage(parameter={m: t.numpy() for m, t in p.items()}, aggregation_weight=w))
+    got = algo.aggregate_worker_data().parameter
+    want = oracle.aggregate_worker_data().parameter
+    for name, v in want.items():
+        assert bits_equal(got[name].cpu().numpy(), v), name
+    algo.exit()

@@ -1049,6 +1049,7 @@ def main_plugin(args: argparse.Namespace) -> int:
     ctx.prof_enable(not args.no_kernel_events)
     host_s[0] = 0.0
     dyn0 = dict(algo.dyn_stats)
+    ctx.dyn_prof_collect()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -1057,6 +1058,7 @@ def main_plugin(args: argparse.Namespace) -> int:
     elapsed = time.perf_counter() - t0
     ctx.prof_enable(False)
     kernel_ms, launches = ctx.prof_collect()
+    dyn_ms, dyn_waves = ctx.dyn_prof_collect()
     dyn = {k: round((algo.dyn_stats[k] - dyn0[k]) / args.steps, 2) for k in dyn0}
     in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
     job_bytes = N * P * in_b + P * out_b
@@ -1067,6 +1069,13 @@ def main_plugin(args: argparse.Namespace) -> int:
     step_s = elapsed / args.steps
     kstep_s = kernel_ms * 1e-3 / args.steps
     achieved = launch_bytes / kstep_s / 1e9 if kstep_s > 0 else 0.0
+    dyn_rows_all = dyn_waves and dyn["rows"] == N and dyn["finalized"] == 1
+    if dyn_rows_all:
+        # every row folded by the round's dynamic wave: its body launch (enqueue at the first
+        # arrival to its end, arrival phase included) carries the round's bytes
+        kstep_s = dyn_ms * 1e-3 / args.steps
+        launch_bytes = job_bytes
+        achieved = launch_bytes / kstep_s / 1e9 if kstep_s > 0 else 0.0
     cpu = None
     if not args.no_cpu_baseline:
         del params, views, buckets
@@ -1107,8 +1116,10 @@ def main_plugin(args: argparse.Namespace) -> int:
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": f"fedavg_tile_kernel x {n_waves} launch(es) per round", "bytes_per_step": launch_bytes,
-            "kernel_ms_per_step": round(kstep_s * 1e3, 4), "launches": launches},
+            "kernel": ("dyn_wave_kernel (body launch, enqueued at the first arrival; arrivals included)"
+                       if dyn_rows_all else f"fedavg_tile_kernel x {n_waves} launch(es) per round"),
+            "bytes_per_step": launch_bytes,
+            "kernel_ms_per_step": round(kstep_s * 1e3, 4), "launches": launches + dyn_waves},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -2197,6 +2197,8 @@ struct fedavg_ctx {
     hipStream_t edge_stream = nullptr;  // the edge launch runs beside the body launch
     hipEvent_t edge_done = nullptr;
     bool unjoined = false;  // a finalized wave closed with join = 0: fedavg_check waits for it
+    hipEvent_t prof_start = nullptr;  // profiling: the open of the wave being timed
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof;  // (open, end of the body launch) per wave
     uint32_t epoch = 0;        // waves opened on this context (tags the mirror word)
     hipStream_t stream = nullptr;
     hipEvent_t start = nullptr, done = nullptr;
@@ -3145,6 +3147,11 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
+  for (auto& pr : c->dyn.prof) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (c->dyn.prof_start) (void)hipEventDestroy(c->dyn.prof_start);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->d_tiles1) (void)hipFree(c->d_tiles1);
   if (c->d_tiles4) (void)hipFree(c->d_tiles4);
@@ -4218,6 +4225,12 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   a.epoch = d.epoch;
   a.idle_ticks = d.idle_ticks;
   a.life_ticks = d.life_ticks;
+  d.prof_start = nullptr;
+  if (c->prof) {  // the body launch timed from its enqueue to its end (arrivals included)
+    d.prof_start = take_event(c);
+    if (!d.prof_start) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
+    FEDAVG_HIP_TRY(hipEventRecord(d.prof_start, d.stream));
+  }
   // the body launch (its workgroup 0 is the mirror) first, so its workgroups are resident first
   const dim3 grid(static_cast<unsigned>(a.num_tiles + 1)), block(kDynLanes);
   switch (in_dtype) {
@@ -4326,6 +4339,13 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
   FEDAVG_HIP_TRY(hipSetDevice(c->device));
   // an accumulator close always joins `stream` (the ordinary calls continue from the accumulator)
   const bool joined = join || !(state == 1 && mode != OUT_ACC);
+  if (d.prof_start) {
+    hipEvent_t stop = take_event(c);
+    if (!stop) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
+    FEDAVG_HIP_TRY(hipEventRecord(stop, d.stream));
+    d.prof.emplace_back(d.prof_start, stop);
+    d.prof_start = nullptr;
+  }
   FEDAVG_HIP_TRY(hipEventRecord(d.done, d.stream));
   if (joined) FEDAVG_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), d.done, 0));
   if (!d.edge_tiles.empty()) {
@@ -4361,6 +4381,25 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
   }
   if (folded_out) *folded_out = static_cast<int32_t>(folded);
   if (finalized_out) *finalized_out = finalized ? 1 : 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_prof_collect(fedavg_ctx* c, double* total_ms, int32_t* waves) {
+  FEDAVG_RET(check_ctx(c));
+  double sum = 0.0;
+  for (auto& pr : c->dyn.prof) {
+    FEDAVG_HIP_TRY(hipEventSynchronize(pr.second));
+    float ms = 0.f;
+    FEDAVG_HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    sum += ms;
+  }
+  if (total_ms) *total_ms = sum;
+  if (waves) *waves = static_cast<int32_t>(c->dyn.prof.size());
+  for (auto& pr : c->dyn.prof) {
+    c->event_pool.push_back(pr.first);
+    c->event_pool.push_back(pr.second);
+  }
+  c->dyn.prof.clear();
   return FEDAVG_OK;
 }
 

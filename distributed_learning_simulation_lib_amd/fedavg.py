@@ -681,6 +681,12 @@ class FedAvgContext:
                                                  ctypes.byref(folded), ctypes.byref(fin)))
         return int(folded.value), bool(fin.value)
 
+    def dyn_prof_collect(self) -> tuple[float, int]:
+        """(ms, waves): the closed dynamic waves' body launches, enqueue to end, while profiling."""
+        ms, n = ctypes.c_double(), ctypes.c_int32()
+        _native.check(self._lib.fedavg_dyn_prof_collect(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
     def dyn_state(self) -> tuple[bool, int]:
         a, p = ctypes.c_int32(), ctypes.c_int32()
         _native.check(self._lib.fedavg_dyn_state(self._h, ctypes.byref(a), ctypes.byref(p)))

@@ -484,6 +484,9 @@ int32_t fedavg_dyn_publish(fedavg_ctx* ctx, const void* const* client_ptrs, cons
 int32_t fedavg_dyn_close(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dtype, int32_t join, void* stream,
                          int32_t* folded_out, int32_t* finalized_out);
 int32_t fedavg_dyn_state(const fedavg_ctx* ctx, int32_t* active, int32_t* published);
+/* With fedavg_prof_enable on: the summed time of the closed waves' body launches (enqueue at
+ * the open to the launch's end, so the arrival phase is included) and their count; clears them. */
+int32_t fedavg_dyn_prof_collect(fedavg_ctx* ctx, double* total_ms, int32_t* waves);
 
 /* =====================================================================================
  * Single-process multi-device mode ("a communicator created by the library

@@ -155,7 +155,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         # tensors) or a current stream with unfinished work closes it early: it keeps the rows it
         # folded and the ordinary waves fold the rest, with the same bits.
         self.dynamic_wave = (os.environ.get("FEDAVG_DYN", "1") != "0") if dynamic_wave is None else bool(dynamic_wave)
-        self.__dyn_batch = max(1, int(os.environ.get("FEDAVG_DYN_BATCH", 4)))
+        self.__dyn_batch = max(1, int(os.environ.get("FEDAVG_DYN_BATCH", 2)))
         self.__dyn_table: Any = None         # the table the open dynamic wave reads
         self.__dyn_pub = 0                   # its rows published so far
         self.__dyn_closed: Any = None        # (table, rows folded) of the round's closed dynamic wave

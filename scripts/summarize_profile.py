@@ -43,7 +43,7 @@ alg = K * P * 4 + P * 4
 traffic = fetch_main * 1024 * read_corr + write_main * 1024 * write_corr
 out = {
     "tag": tag,
-    "kernel": "fedavg_tile_kernel<float, OUT_F32, 1, true>",
+    "kernel": "fedavg_tile_kernel<float, OUT_F32, 1, true, fma>",
     "workload": "64 clients x ResNet-18 (62 tensors, 11,689,512 params) fp32 -> fp32, fp64 accumulation",
     "kernel_avg_ms_rocprof": main_avg_ns / 1e6,
     "algorithmic_bytes_per_launch": alg,

@@ -164,6 +164,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         # open / close cost more than the arrivals it hides
         self.dyn_min_rows = int(os.environ.get("FEDAVG_DYN_MIN_ROWS", 4))
         self.__prev_arrivals: int | None = None  # the previous round's process_worker_data calls
+        # the input dtype of the last round's wave: the next round opens its wave with it before
+        # staging its first update (bound to that update's row, or closed empty if it differs)
+        self.__dyn_last: Any = None
+        self.__dyn_pre: Any = None           # the dtype of a wave opened before its first row
+        self.__dyn_pre_ctx: Any = None       # ... and the context it was opened on
         self.__round_updates = 0
         # dynamic waves opened, rows they folded, waves that wrote the round's result themselves
         self.dyn_stats = {"waves": 0, "rows": 0, "finalized": 0}
@@ -385,6 +390,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_data: Message | None,
     ) -> bool:
         self.__round_updates += 1
+        if self.__round_updates == 1 and self.__dyn_last is not None:
+            self._dyn_preopen()
         if worker_data is not None and self._arrive_quick(worker_id, worker_data):
             return True
         res = super().process_worker_data(worker_id, worker_data)
@@ -818,6 +825,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__has_data = True
         if type(self.__table) is NativeClientTable:
             self._dyn_arrival()
+        else:
+            self._dyn_unpre()
 
     def _scan_arrival(self, tensors: list, dt: Any, worker_id: int | None, delta: bool) -> None:
         """fed_avg_algorithm.py:34-35 at the arrival: one GPU scan of the staged update."""
@@ -925,6 +934,30 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return ev is None or ev.query()
 
     # ---- the dynamic wave (fedavg_dyn_*) ------------------------------------------------
+    def _dyn_preopen(self) -> None:
+        """The round's first update is arriving: open the wave with the last round's input dtype
+        now, so the launch overlaps this update's staging (its row binds it in _dyn_arrival)."""
+        if not (self.dynamic_wave and self.device.type == "cuda" and self.__multi_devices is None
+                and self.accumulate and self.__default_hooks and not self.wave_min and not self.eager_nan_check
+                and self.__table is None and not self.__dyn_round and self.__dyn_table is None
+                and (self.__prev_arrivals is None or self.__prev_arrivals >= self.dyn_min_rows)):
+            return
+        ctx = self._context()
+        try:
+            ctx.dyn_open(self.__dyn_last, self.wave_size)
+        except _native.NativeError:
+            return
+        self.__dyn_pre, self.__dyn_pre_ctx = self.__dyn_last, ctx
+
+    def _dyn_unpre(self) -> None:
+        """Close a wave opened before its first row that no row will bind (it folded nothing)."""
+        if self.__dyn_pre is not None:
+            ctx, self.__dyn_pre, self.__dyn_pre_ctx = self.__dyn_pre_ctx, None, None
+            try:
+                ctx.dyn_close(None)
+            except _native.NativeError:
+                pass  # its context was replaced (a grown layout): closing it ended the wave
+
     def _dyn_arrival(self) -> None:
         """A row joined the wave's native table: open the round's dynamic wave at the first one
         (when the round qualifies), then hand it the staged rows every ``FEDAVG_DYN_BATCH``."""
@@ -939,11 +972,19 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     and not self.wave_min and not self.eager_nan_check and self.__ew is False
                     and not self.__table_delta and self.__table_dtype in _DYN_DTYPES
                     and (self.__prev_arrivals is None or self.__prev_arrivals >= self.dyn_min_rows)):
+                self._dyn_unpre()
+                self.__dyn_last = None
                 return
-            try:
-                self._context().dyn_open(self.__table_dtype, self.wave_size)
-            except _native.NativeError:
-                return  # e.g. the accumulator already holds data: the ordinary waves
+            if self.__dyn_pre is not None and (self.__dyn_pre != self.__table_dtype
+                                               or self.__dyn_pre_ctx is not self._context()):
+                self._dyn_unpre()  # opened for another dtype or context: reopen for this one
+            if self.__dyn_pre is None:
+                try:
+                    self._context().dyn_open(self.__table_dtype, self.wave_size)
+                except _native.NativeError:
+                    return  # e.g. the accumulator already holds data: the ordinary waves
+            self.__dyn_pre = self.__dyn_pre_ctx = None
+            self.__dyn_last = self.__table_dtype
             self.__dyn_table, self.__dyn_pub, self.__dyn_closed = table, 0, None
             self.dyn_stats["waves"] += 1
         elif self.__dyn_table is not table:
@@ -982,6 +1023,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
 
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""
+        self._dyn_unpre()
         if self.__table is None or self.__table.num_clients == 0:
             return
         ctx = self._context()
@@ -1039,6 +1081,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return out
 
     def _reset_round(self) -> None:
+        try:
+            self._dyn_unpre()
+        except _native.NativeError:
+            self.__dyn_pre = None
         if self.__dyn_table is not None:  # an abandoned round's dynamic wave ends with its rows
             try:
                 self._dyn_close(None)
@@ -1077,6 +1123,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return moved
 
     def _finish_native(self) -> ModelParameter:
+        self._dyn_unpre()
         if self.__multi_devices is not None:
             if not self.__ew:
                 return self._finish_multi()

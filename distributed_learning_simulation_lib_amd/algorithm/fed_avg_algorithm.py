@@ -1124,6 +1124,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
 
     def _finish_native(self) -> ModelParameter:
         self._dyn_unpre()
+        if self.__dyn_table is not None and self.__dyn_table is self.__table:
+            self._dyn_publish()  # the last rows to the wave first: it folds them while the result is prepared
         if self.__multi_devices is not None:
             if not self.__ew:
                 return self._finish_multi()
@@ -1149,11 +1151,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self.__result_flat = None if custom_divide else flat
         delta = self.__table_delta and table is not None
         done = False  # the dynamic wave wrote the result
-        if table is not None and self.__dyn_table is table:
-            if self.__dyn_pub < table.num_clients and not torch.cuda.current_stream(self.device).query():
-                # the last arrivals' copies / conversions are still running: wait for them, as
-                # the one-launch path would, so the wave can take every row
-                torch.cuda.current_stream(self.device).synchronize()
+        if table is not None and self.__dyn_table is table and self.__dyn_pub < table.num_clients:
+            # the last arrivals' copies / conversions were still running at the first publication:
+            # wait for them, as the one-launch path would, so the wave can take every row
+            torch.cuda.current_stream(self.device).synchronize()
             self._dyn_publish()  # (a row it cannot take closes the wave here: the rest below)
         if table is not None and self.__dyn_table is table and self.__dyn_pub < table.num_clients:
             self._dyn_close(None)  # rows left unpublished: the wave keeps its rows, the rest below

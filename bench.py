@@ -1126,6 +1126,85 @@ def main_plugin(args: argparse.Namespace) -> int:
     return 0
 
 
+SPEEDUP_TARGET = {4: 3.5}  # BASELINE.json north_star: >= 3.5x at 4 GPUs (strong scaling, config 3)
+
+
+def one_gpu_anchor(layout: ModelLayout, n_total: int, weights: list, in_dtype: torch.dtype, out_dtype: torch.dtype,
+                   device: torch.device, steps: int, warmup: int, resident: list | None = None) -> dict:
+    """The same n_total-client job on ``device`` alone with the N = 1 fused kernel, timed like the
+    one-GPU line (one plan launch + the NaN readback per round, bench.py --gpus 1 --total-clients
+    n_total): the anchor of an N > 1 line's measured speed-up, taken in the same run. ``resident``:
+    (first client, row views) already on ``device`` (the shard of entry 0, or every shard of an
+    aliased rehearsal); the other clients are generated there from their seeds."""
+    T = layout.num_segments
+    have = {first + i: row for first, views in (resident or []) for i, row in enumerate(views)}
+    made, rows, c = [], [], 0
+    while c < n_total:
+        if c in have:
+            rows.append(have[c])
+            c += 1
+            continue
+        stop = c
+        while stop < n_total and stop not in have:
+            stop += 1
+        buckets, views = make_clients(layout, c, stop - c, device, in_dtype)
+        made.append(buckets)
+        rows.extend(views)
+        c = stop
+    table = ClientTable(T)
+    for row, w in zip(rows, weights):
+        table.add_client(row, [w] * T)
+    ctx = FedAvgContext(layout, device)
+    offs, padded = layout.padded_offsets(out_dtype.itemsize)
+    flat = torch.empty(padded, dtype=out_dtype, device=device)
+    outs = OutputTable([flat[o : o + n] for o, n in zip(offs, layout.numels)], layout, device, out_dtype)
+    reducer = HipLocalReducer(ctx, table, in_dtype, outs, out_dtype)
+
+    def step() -> None:
+        reducer.fused()
+        reducer.raise_on_nan()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(device)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    generated = sum(b.numel() * b.element_size() for b in made)
+    del reducer, table, made, rows
+    ctx.close()
+    torch.cuda.empty_cache()
+    return {"anchor_ms_per_step": round(ms, 4), "anchor_device": str(device), "anchor_clients": n_total,
+            "anchor_clients_generated_bytes": generated}
+
+
+def speedup_block(G: int, ms_per_step: float | None, anchor: dict | None, aliased: bool,
+                  tail: tuple[float, float, int] | None = None, predicted: dict | None = None) -> dict:
+    """The N > 1 line's own verdict on the north-star speed-up: the same-N one-GPU anchor timed in
+    this run, measured_speedup = anchor / ms_per_step, the target for this G, and the exposed
+    exchange tail measured with events beside the cost model's. An aliased rehearsal (every entry
+    on one GPU) reports its ratio as ``aliased_ratio`` only: it is not a scaling figure."""
+    a = None if anchor is None else anchor["anchor_ms_per_step"]
+    ratio = None if a is None or not ms_per_step else round(a / ms_per_step, 3)
+    target = SPEEDUP_TARGET.get(G)
+    out = {"anchor": anchor, "measured_speedup": None if aliased else ratio,
+           "aliased_ratio": ratio if aliased else None, "target_speedup": target,
+           "meets_target": None if aliased or ratio is None or target is None else bool(ratio >= target),
+           "basis": ("aliased rehearsal: every entry on one GPU, not a scaling figure" if aliased else
+                     "measured: the same clients on device 0 alone vs this line's step, one run")}
+    if tail is not None:
+        fold, tl, n = tail
+        out["events"] = {"rounds": n, "entry0_fold_ms": None if not n else round(fold / n, 4),
+                         "exposed_exchange_and_finalize_ms": None if not n else round(tl / n, 4),
+                         "predicted_exposed_exchange_and_finalize_ms":
+                             None if predicted is None else predicted.get("exposed_exchange_and_finalize_ms"),
+                         "what": "entry 0's stream: round start -> its last chunk fold -> the round's end behind "
+                                 "every exchange (fedavg_multi_prof_*), over rounds after the timed ones"}
+    return out
+
+
 def main_multi(args: argparse.Namespace) -> int:
     """--procs 1 --gpus N: ONE process drives N GPUs through the single-process multi-device mode
     (include/fedavg_hip.h fedavg_multi_*) — the structure of the reference's single
@@ -1157,12 +1236,13 @@ def main_multi(args: argparse.Namespace) -> int:
         m.close()
         return 3
     _STAGES.enter("make_clients")
-    keep, tables = [], []
+    keep, tables, rows_of = [], [], []
     for g, d in enumerate(devices):
         lo, hi = shard_bounds(n_total, G, g)
         dev = torch.device("cuda", d)
         buckets, views = make_clients(layout, lo, hi - lo, dev, in_dtype)
         keep.append(buckets)
+        rows_of.append((lo, views))
         t = ClientTable(T)
         for row, w in zip(views, weights_all[lo:hi]):
             t.add_client(row, [w] * T)
@@ -1262,8 +1342,24 @@ def main_multi(args: argparse.Namespace) -> int:
     achieved = rank_bytes / (kernel_step_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     predicted = model.round_ms(G, P, n_total, in_b, out_b, edges, ex) if G > 1 else None
     one_gpu = model.one_gpu_ms(P, n_total, in_b, out_b)
+    # the exposed exchange + division tail, event-timed on entry 0 over the same number of rounds
+    _STAGES.enter("exchange_tail")
+    m.prof_collect()
+    m.prof_enable(True)
+    for _ in range(args.steps):
+        one_round(ex, edges)
+    sync_all()
+    m.prof_enable(False)
+    tail = m.prof_collect()
     _STAGES.enter("teardown")
     m.close()
+    del partials
+    # the same N-client job on device 0 alone, N = 1 kernel, same steps and warmup
+    _STAGES.enter("anchor", args.stage_timeout + 120)
+    anchor = None if args.no_anchor else one_gpu_anchor(
+        layout, n_total, weights_all, in_dtype, out_dtype, root_dev, args.steps, args.warmup,
+        resident=[r for g, r in enumerate(rows_of) if devices[g] == devices[0]])
+    speed = speedup_block(G, step_s * 1e3, anchor, args.alias, tail, predicted)
     _STAGES.enter("done", 0)
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": len(set(devices)), "steps": args.steps,
@@ -1296,6 +1392,7 @@ def main_multi(args: argparse.Namespace) -> int:
             "bytes_per_step_this_rank": rank_bytes, "kernel_ms_per_step": round(kernel_step_ms, 4),
             "launches": launches,
         },
+        "speedup": speed,
         "result_check": check,
         "cpu_baseline": None,
     }
@@ -1498,6 +1595,7 @@ def main_dry_one_process(args: argparse.Namespace) -> int:
                    "exchange": {"mode": ex, "chunks": ch, "chunk_shape": sh, "selection": "cost model",
                                 "predicted_speedup": pred["speedup"]},
                    "launched_by": os.environ.get("BENCH_LAUNCHED_BY", "none")},
+        "speedup": speedup_block(G, None, None, args.alias, (0.0, 0.0, 0), pred),
         "dry_run": "launcher check on the CPU: the single-process run's skeleton; not a measurement",
     }
     print(json.dumps(line), flush=True)
@@ -1556,6 +1654,8 @@ def main_dry(args: argparse.Namespace) -> int:
         "dry_run": "launcher check on the CPU: rank processes, gloo group, shards, max-over-ranks timing; "
                    "not a measurement",
     }
+    if world > 1:
+        line["speedup"] = speedup_block(world, None, None, args.rehearse)
     if os.environ.get("BENCH_LAUNCH_FALLBACK"):
         line["config"]["launch_fallback"] = os.environ["BENCH_LAUNCH_FALLBACK"]
     print(json.dumps(line), flush=True)
@@ -1698,6 +1798,9 @@ def main() -> int:
     ap.add_argument("--one-process-timeout", type=float, default=200.0,
                     help="--gpus N > 1 (default launch): seconds the one-process run may take before the "
                          "launcher stops it and starts the per-process ranks (capped at half --launch-timeout)")
+    ap.add_argument("--no-anchor", action="store_true",
+                    help="N > 1: skip timing the same-N job on GPU 0 alone after the timed region (the "
+                         "line's measured_speedup is then null)")
     ap.add_argument("--alias", action="store_true",
                     help="--procs 1: every device entry on cuda:0 (a one-GPU rehearsal of the multi-device round)")
     ap.add_argument("--multi-exchange", default="peer", choices=["peer", "reduce"],
@@ -1953,6 +2056,18 @@ def main() -> int:
             p_el = float(pt.item())
         partial_only_ms = p_el / args.steps * 1e3
 
+    # N > 1: the same N-client job on rank 0's GPU alone (N = 1 kernel, same steps and warmup),
+    # timed in this run while the other ranks wait, so the line carries its own measured speed-up
+    anchor = None
+    if world > 1 and not args.no_anchor:
+        _STAGES.enter("anchor", args.stage_timeout + 120)
+        torch.cuda.synchronize(device)
+        if rank == 0:
+            anchor = one_gpu_anchor(layout, n_total, weights_all, in_dtype, out_dtype, device, args.steps,
+                                    args.warmup, resident=[(lo, views)])
+        if dist.is_initialized():
+            dist.barrier()
+
     traffic, traffic_src = (None, None)
     if not sharded and n_waves == 1 and args.layout == "resnet18":
         traffic, traffic_src = committed_traffic(world, n_local, args.in_dtype, args.out_dtype)
@@ -2056,6 +2171,8 @@ def main() -> int:
         },
         # the input-only form N·P·s_in / t beside the algorithmic-bytes value
         "input_only_GBps": round(n_total * P * in_bytes / step_s / 1e9, 2),
+        **({"speedup": speedup_block(world, step_s * 1e3, anchor, args.rehearse, None, predicted)}
+           if world > 1 else {}),
         "host_enqueue_ms_per_step": round(host_enqueue[0] * 1e3 / args.steps, 4),
         "hbm_probe": probe,
         "result_check": check,

@@ -167,6 +167,8 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_multi_check": (c_int32, [c_void_p, POINTER(c_uint32)]),
     "fedavg_multi_round_check": (c_int32, [c_void_p, POINTER(c_uint32)]),
     "fedavg_multi_reset": (c_int32, [c_void_p]),
+    "fedavg_multi_prof_enable": (c_int32, [c_void_p, c_int32]),
+    "fedavg_multi_prof_collect": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_int32)]),
 }
 
 _lib: ctypes.CDLL | None = None

@@ -117,6 +117,11 @@ struct fedavg_multi {
   std::vector<char*> comb_dev;
   std::vector<std::vector<char>> comb_host;
   bool any_round = false;
+  // fedavg_multi_prof_enable: per round, three timing events on entry 0's stream (device 0) — the
+  // round's start, the end of entry 0's last chunk fold, the round's end behind every exchange
+  bool prof = false;
+  std::vector<std::vector<hipEvent_t>> prof_ev;  // rounds x {start, fold end, end}
+  std::vector<hipEvent_t> prof_pool;
   // in-process RCCL (REDUCE exchange)
   std::vector<ncclComm_t> nccl;
 };
@@ -135,6 +140,23 @@ int32_t ensure_part_events(fedavg_multi* m, int32_t chunks) {
       m->part_ev[g].push_back(ev);
     }
   }
+  return FEDAVG_OK;
+}
+
+// fedavg_multi_prof_enable: a timing event recorded on entry 0's stream (device 0)
+int32_t prof_mark(fedavg_multi* m, void* const* streams, int32_t which) {
+  if (!m->prof) return FEDAVG_OK;
+  MULTI_HIP_TRY(hipSetDevice(m->devices[0]));
+  if (which == 0) m->prof_ev.push_back(std::vector<hipEvent_t>(3, nullptr));
+  hipEvent_t ev = nullptr;
+  if (!m->prof_pool.empty()) {
+    ev = m->prof_pool.back();
+    m->prof_pool.pop_back();
+  } else {
+    MULTI_HIP_TRY(hipEventCreate(&ev));
+  }
+  m->prof_ev.back()[which] = ev;
+  MULTI_HIP_TRY(hipEventRecord(ev, (streams && streams[0]) ? static_cast<hipStream_t>(streams[0]) : m->own[0]));
   return FEDAVG_OK;
 }
 
@@ -484,6 +506,12 @@ int32_t fedavg_multi_destroy(fedavg_multi* m) {
     if (m->start_ev[j]) (void)hipEventDestroy(m->start_ev[j]);
     if (m->done_ev[j]) (void)hipEventDestroy(m->done_ev[j]);
     if (j == 0 && m->end_ev) (void)hipEventDestroy(m->end_ev);
+    if (j == 0) {
+      for (auto& r : m->prof_ev)
+        for (hipEvent_t ev : r)
+          if (ev) (void)hipEventDestroy(ev);
+      for (hipEvent_t ev : m->prof_pool) (void)hipEventDestroy(ev);
+    }
     if (m->own[j]) (void)hipStreamDestroy(m->own[j]);
     if (m->xstr[j]) (void)hipStreamDestroy(m->xstr[j]);
     if (m->ctx[j]) (void)fedavg_ctx_destroy(m->ctx[j]);
@@ -539,6 +567,9 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
     if (int32_t st = upload_windows(m, edges)) return st;
     if (int32_t st = upload_comb(m, members, chunks)) return st;
     if (int32_t st = order_round_start(m, streams)) return st;
+    if (int32_t st = prof_mark(m, streams, 0)) return st;
+    if (partials[0] == nullptr)
+      if (int32_t st = prof_mark(m, streams, 1)) return st;  // entry 0 folds nothing
     const int32_t vec = outs_aligned(out_ptrs, m->T, out_dtype) ? 1 : 0;
     // a member with a dense plan folds its own window last, with the other members' partials of
     // it added in entry order in the same kernel (no own-window slot store and re-read)
@@ -583,6 +614,8 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
         }
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
         MULTI_HIP_TRY(hipEventRecord(m->part_ev[g][k], s));
+        if (g == 0 && k == chunks - 1)
+          if (int32_t st = prof_mark(m, streams, 1)) return st;
       }
       for (int32_t j = 0; j < m->G; ++j) {
         int32_t wb = 0, we = 0;
@@ -609,12 +642,14 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
           return st;
       }
     }
-    return order_round_end(m, streams);
+    if (int32_t st = order_round_end(m, streams)) return st;
+    return prof_mark(m, streams, 2);
   }
   if (exchange == FEDAVG_EXCHANGE_REDUCE) {
     if (int32_t st = ensure_nccl(m)) return st;
     if (int32_t st = ensure_part_events(m, chunks)) return st;
     if (int32_t st = order_round_start(m, streams)) return st;
+    if (int32_t st = prof_mark(m, streams, 0)) return st;
     for (int32_t k = 0; k < chunks; ++k) {
       for (int32_t g = 0; g < m->G; ++g) {
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
@@ -629,13 +664,16 @@ int32_t fedavg_multi_round(fedavg_multi* m, fedavg_plan* const* partials, const 
         MULTI_HIP_TRY(hipSetDevice(m->devices[g]));
         MULTI_HIP_TRY(hipEventRecord(m->part_ev[g][k], s));
         MULTI_HIP_TRY(hipStreamWaitEvent(m->xstr[g], m->part_ev[g][k], 0));
+        if (g == 0 && k == chunks - 1)
+          if (int32_t st = prof_mark(m, streams, 1)) return st;
       }
       int64_t a = 0, b = 0;
       if (int32_t st = fedavg_tile_range(m->ctx[0], edges[k], edges[k + 1], &a, &b)) return st;
       if (int32_t st = grouped_reduce(m, a, b, root)) return st;
     }
     if (int32_t st = root_finalize(m, total_weights, out_ptrs, out_dtype, root)) return st;
-    return order_round_end(m, streams);
+    if (int32_t st = order_round_end(m, streams)) return st;
+    return prof_mark(m, streams, 2);
   }
   return invalid("exchange must be FEDAVG_EXCHANGE_PEER or FEDAVG_EXCHANGE_REDUCE");
 }
@@ -735,6 +773,38 @@ int32_t fedavg_multi_round_check(fedavg_multi* m, uint32_t* flags_out) {
   if (flags_out) *flags_out = f;
   if (f & FEDAVG_FLAG_ACC_NAN) return fedavg_internal_fail(FEDAVG_ERR_NAN_ACCUM, "NaN in the accumulator");
   if (f & FEDAVG_FLAG_RESULT_NAN) return fedavg_internal_fail(FEDAVG_ERR_NAN_RESULT, "NaN in the aggregated result");
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_multi_prof_enable(fedavg_multi* m, int32_t on) {
+  if (!m) return invalid("null multi-device object");
+  m->prof = on != 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_multi_prof_collect(fedavg_multi* m, double* fold_ms, double* tail_ms, int32_t* rounds) {
+  DeviceRestore restore_device;
+  if (!m) return invalid("null multi-device object");
+  double fold = 0.0, tail = 0.0;
+  int32_t n = 0;
+  MULTI_HIP_TRY(hipSetDevice(m->devices[0]));
+  for (auto& r : m->prof_ev) {
+    if (!r[0] || !r[1] || !r[2]) continue;  // a round that failed while enqueuing
+    MULTI_HIP_TRY(hipEventSynchronize(r[2]));
+    float a = 0.f, b = 0.f;
+    MULTI_HIP_TRY(hipEventElapsedTime(&a, r[0], r[1]));
+    MULTI_HIP_TRY(hipEventElapsedTime(&b, r[1], r[2]));
+    fold += a;
+    tail += b;
+    ++n;
+  }
+  for (auto& r : m->prof_ev)
+    for (hipEvent_t ev : r)
+      if (ev) m->prof_pool.push_back(ev);
+  m->prof_ev.clear();
+  if (fold_ms) *fold_ms = fold;
+  if (tail_ms) *tail_ms = tail;
+  if (rounds) *rounds = n;
   return FEDAVG_OK;
 }
 

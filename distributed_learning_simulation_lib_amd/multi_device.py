@@ -151,6 +151,18 @@ class MultiDeviceContext:
     def reset(self) -> None:
         _native.check(self._lib.fedavg_multi_reset(self._h))
 
+    def prof_enable(self, on: bool = True) -> None:
+        """Time every following round with events on entry 0's stream (fedavg_multi_prof_enable)."""
+        _native.check(self._lib.fedavg_multi_prof_enable(self._h, 1 if on else 0))
+
+    def prof_collect(self) -> tuple[float, float, int]:
+        """(fold ms, tail ms, rounds) summed over the rounds timed since the last collect: entry 0's
+        round start -> its last chunk fold, and that fold -> the round's end behind every exchange."""
+        fold, tail, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+        _native.check(self._lib.fedavg_multi_prof_collect(self._h, ctypes.byref(fold), ctypes.byref(tail),
+                                                          ctypes.byref(n)))
+        return float(fold.value), float(tail.value), int(n.value)
+
     def raise_on_nan(self, pending: Sequence[Sequence[tuple[ClientTable, torch.dtype]]] = (),
                      round_only: bool = False) -> None:
         """The reference's assertions (fed_avg_algorithm.py:35,93,97) for the whole round: an input

@@ -554,6 +554,16 @@ int32_t fedavg_multi_combine(fedavg_multi* m, const double* total_weights, void*
 int32_t fedavg_multi_check(fedavg_multi* m, uint32_t* flags_out);
 int32_t fedavg_multi_round_check(fedavg_multi* m, uint32_t* flags_out);
 int32_t fedavg_multi_reset(fedavg_multi* m);
+/* Measurement of fedavg_multi_round (bench.py's N > 1 line): while enabled, every round records
+ * three timing events on entry 0's stream (device 0) — the round's start, the end of entry 0's
+ * last chunk fold (its client reads; the peer stores of its other windows), and the round's end
+ * behind every entry's exchange work. fedavg_multi_prof_collect waits for them and returns the
+ * summed fold and tail (fold end -> round end: the exposed exchange + division that the
+ * reference's single server process, simulation_lib/server/server.py:122-152, waits for after the
+ * last fold) times in ms over the recorded rounds, then clears them. The markers sit between the
+ * round's launches, so time profiled rounds apart from the timed ones. */
+int32_t fedavg_multi_prof_enable(fedavg_multi* m, int32_t on);
+int32_t fedavg_multi_prof_collect(fedavg_multi* m, double* fold_ms, double* tail_ms, int32_t* rounds);
 
 #ifdef __cplusplus
 }

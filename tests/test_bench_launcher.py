@@ -48,6 +48,14 @@ def test_default_launch_is_one_process_driving_every_gpu(world, shards):
     assert line["config"]["exchange"]["mode"] == "peer"
     assert line["config"]["exchange"]["predicted_speedup"] > 1.0
     assert "launch_fallback" not in line["config"]
+    # every N > 1 line judges the north-star speed-up itself: the same-N one-GPU anchor timed in
+    # the run, measured_speedup = anchor / ms_per_step, the event-timed exchange tail
+    sp = line["speedup"]
+    for key in ("anchor", "measured_speedup", "aliased_ratio", "target_speedup", "meets_target", "basis", "events"):
+        assert key in sp, key
+    assert sp["target_speedup"] == (3.5 if world == 4 else None)
+    for key in ("entry0_fold_ms", "exposed_exchange_and_finalize_ms", "predicted_exposed_exchange_and_finalize_ms"):
+        assert key in sp["events"], key
 
 
 def test_failed_one_process_run_falls_back_to_fresh_rank_processes():
@@ -108,6 +116,7 @@ def test_launcher_spawns_ranks_and_relays_one_line(world, shards):
     assert line["config"]["client_shards"] == shards
     assert line["config"]["launched_by"] == "bench.py"
     assert line["scaling"] == "strong" and line["steps"] == 3 and line["warmup"] == 1
+    assert {"anchor", "measured_speedup", "aliased_ratio", "target_speedup", "meets_target"} <= set(line["speedup"])
 
 
 def test_one_gpu_runs_in_process():
@@ -242,3 +251,26 @@ def test_watchdog_fails_a_torchrun_job_fast():
     # stops the other
     assert "stage 'timed' still running after 5 s" in r.stderr
     assert _time.monotonic() - t0 < 120
+
+
+def test_speedup_block_labels_aliased_ratios():
+    import importlib.util
+    import sys as _sys
+
+    spec = importlib.util.spec_from_file_location("bench_mod", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    argv = _sys.argv
+    _sys.argv = ["bench.py"]
+    try:
+        spec.loader.exec_module(bench)
+    finally:
+        _sys.argv = argv
+    anchor = {"anchor_ms_per_step": 1.9}
+    real = bench.speedup_block(4, 0.5, anchor, aliased=False, tail=(1.0, 0.2, 4), predicted={
+        "exposed_exchange_and_finalize_ms": 0.03})
+    assert real["measured_speedup"] == 3.8 and real["aliased_ratio"] is None and real["meets_target"] is True
+    assert real["events"]["exposed_exchange_and_finalize_ms"] == 0.05
+    assert real["events"]["predicted_exposed_exchange_and_finalize_ms"] == 0.03
+    fake = bench.speedup_block(4, 1.0, anchor, aliased=True)
+    assert fake["measured_speedup"] is None and fake["aliased_ratio"] == 1.9 and fake["meets_target"] is None
+    assert "not a scaling figure" in fake["basis"]

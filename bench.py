@@ -583,27 +583,46 @@ def host_cpu() -> dict:
     return out
 
 
-def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dtype: torch.dtype = torch.float32) -> dict:
-    """The reference's CPU path on the host cores, rank 0, N=1 (BASELINE.md §4): the reference's
-    FedAVGAlgorithm call sequence (oracle/ref_torch_cpu.py: process_worker_data per client with
-    its torch CPU ops, then aggregate_worker_data) over ``n_clients`` pre-built messages of the
-    headline workload (64 x ResNet-18 fp32, dataset-size weights), best of ``repeats``."""
+def gpu_local_cpus(device_index: int = 0) -> tuple[list[int], str]:
+    """CPUs on the GPU's own NUMA node (sysfs ``local_cpulist`` of its PCI function), among those this
+    process may use — where a CPU baseline beside this GPU's job should run — and where they came from."""
+    usable = sorted(os.sched_getaffinity(0))
+    try:
+        pr = torch.cuda.get_device_properties(device_index)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        text = Path(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read_text().strip()
+    except (AttributeError, OSError, RuntimeError, AssertionError):
+        return usable, "affinity mask (the GPU's NUMA node is not readable here)"
+    local: set[int] = set()
+    for part in text.split(","):
+        lo, _, hi = part.partition("-")
+        local.update(range(int(lo), int(hi or lo) + 1))
+    mine = [c for c in usable if c in local]
+    return (mine, f"local_cpulist of the GPU's PCI function {bdf}") if mine else (usable, "affinity mask")
+
+
+def _cpu_baseline_child(spec: dict) -> dict:
+    """Runs in a fresh process (bench.py --cpu-baseline-child): pinned to the chosen CPUs before torch
+    starts its thread pool, then the reference's round timed ``repeats`` times."""
+    os.sched_setaffinity(0, spec["cpus"])
+    torch.set_num_threads(spec["threads"])
     sys.path.insert(0, str(REPO))
     from distributed_learning_simulation_lib_amd.message import ParameterMessage
     from oracle.ref_torch_cpu import RefFedAvgAlgorithm
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    torch.set_num_threads(threads)
+    layout = LAYOUTS[spec["layout"]]()
+    dtype = getattr(torch, spec["dtype"])
+    n_clients = spec["clients"]
     weights = dataset_size_weights(n_clients)
     clients = []
     for i in range(n_clients):  # generation is outside the timed region
         g = torch.Generator().manual_seed(1234 + i)
         clients.append({n: torch.randn(s, generator=g, dtype=torch.float32).to(dtype)
                         for n, s in zip(layout.names, layout.shapes)})
-    nbytes = n_clients * layout.total_numel * dtype.itemsize + layout.total_numel * 4
     times = []
     t_start = time.perf_counter()
-    for _ in range(repeats):
+    load0 = os.getloadavg()
+    while len(times) < spec["repeats"] and (len(times) < 3 or time.perf_counter() - t_start < spec["budget_s"]):
         msgs = [ParameterMessage(parameter=dict(c), aggregation_weight=w) for c, w in zip(clients, weights)]
         algo = RefFedAvgAlgorithm()
         t0 = time.perf_counter()
@@ -612,7 +631,36 @@ def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dty
         out = algo.aggregate_worker_data()
         times.append(time.perf_counter() - t0)
         del out, algo, msgs
-    best = min(times)
+    return {"times_s": times, "wall_s": time.perf_counter() - t_start, "loadavg_before": load0,
+            "loadavg_after": os.getloadavg(), "threads_seen": torch.get_num_threads()}
+
+
+def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 5, dtype: torch.dtype = torch.float32,
+                 budget_s: float = 20.0) -> dict:
+    """The reference's CPU path on the host cores, rank 0, N=1 (BASELINE.md §4): the reference's
+    FedAVGAlgorithm call sequence (oracle/ref_torch_cpu.py: process_worker_data per client with
+    its torch CPU ops, then aggregate_worker_data) over ``n_clients`` pre-built messages of the
+    headline workload (64 x ResNet-18 fp32, dataset-size weights). Timed in a fresh child process
+    pinned to OMP_NUM_THREADS of the GPU's NUMA-local CPUs (the harness's per-GPU share) before
+    torch starts its thread pool; the value is the best round, with min / median / max of the
+    repeats and the host's load average beside it (the host is shared with other GPUs' jobs)."""
+    import subprocess
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cpus, source = gpu_local_cpus(torch.cuda.current_device() if torch.cuda.is_available() else 0)
+    pinned = cpus[:threads]
+    spec = {"layout": next(k for k, f in LAYOUTS.items() if f().names == layout.names), "clients": n_clients,
+            "dtype": str(dtype).split(".")[-1], "repeats": repeats, "budget_s": budget_s, "threads": threads,
+            "cpus": pinned}
+    load_parent = os.getloadavg()
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--cpu-baseline-child", json.dumps(spec)],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed ({r.returncode}): {r.stderr[-2000:]}")
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    times = sorted(res["times_s"])
+    best, med = times[0], times[len(times) // 2]
+    nbytes = n_clients * layout.total_numel * dtype.itemsize + layout.total_numel * 4
     return {
         "value": round(nbytes / best / 1e9, 3),
         "unit": "GB/s",
@@ -620,11 +668,18 @@ def cpu_baseline(layout: ModelLayout, n_clients: int = 64, repeats: int = 3, dty
         "kind": "port",
         "host_cpu": host_cpu(),
         "seconds_per_round": round(best, 4),
+        "repeats": {"n": len(times), "min_s": round(times[0], 4), "median_s": round(med, 4),
+                    "max_s": round(times[-1], 4), "median_GBps": round(nbytes / med / 1e9, 3)},
+        "pinning": {"cpus": pinned, "source": source, "threads_seen": res["threads_seen"]},
+        "host_load": {"loadavg_1_5_15_before": [round(x, 2) for x in load_parent],
+                      "loadavg_1_5_15_during": [round(x, 2) for x in res["loadavg_after"]],
+                      "machine_cpus": os.cpu_count()},
         "sample": (
             f"the full round: {n_clients} pre-built ParameterMessages x {layout.num_segments}-tensor layout "
             f"({layout.total_numel:,} {str(dtype).split('.')[-1]} params), the reference's FedAVGAlgorithm call sequence "
             f"(process_worker_data x {n_clients}: isnan, to(f64)*w, +=; aggregate_worker_data: isnan, /W, isnan) "
-            f"in torch CPU ops, best of {repeats} ({time.perf_counter() - t_start:.1f} s)"
+            f"in torch CPU ops, best of {len(times)} in a child process pinned to {len(pinned)} CPUs ({source}), "
+            f"{threads} threads ({res['wall_s']:.1f} s)"
         ),
     }
 
@@ -1032,13 +1087,29 @@ def main_plugin(args: argparse.Namespace) -> int:
                 for p, w in zip(params, weights))
 
     host_s = [0.0]
+    # --arrival bursts:K:GAP_MS — the reference server's cadence (server.py:133-146): it polls every
+    # worker, hands what arrived to the algorithm back to back, then sleeps; here K bursts of N/K
+    # updates with GAP_MS of host time between them. The latency its loop sees is the last
+    # arrival -> the result (aggregate_worker_data returning on the host).
+    bursts, gap_s = 1, 0.0
+    if args.arrival != "all":
+        kind, k_s, g_s = args.arrival.split(":")
+        assert kind == "bursts", args.arrival
+        bursts, gap_s = int(k_s), float(g_s) / 1e3
+        assert 1 <= bursts <= N and N % bursts == 0, "bursts must divide the clients"
+    per_burst = N // bursts
+    tail_s = [0.0]
 
     def step() -> None:
         h0 = time.perf_counter()
         for wid, m in enumerate(messages()):
+            if wid and wid % per_burst == 0 and gap_s:
+                time.sleep(gap_s)
             algo.process_worker_data(wid, m)
-        host_s[0] += time.perf_counter() - h0
+        t_last = time.perf_counter()
+        host_s[0] += t_last - h0
         res = algo.aggregate_worker_data()  # ends on the host: the NaN flags are read (:93, :97)
+        tail_s[0] += time.perf_counter() - t_last
         algo.clear_worker_data()
         assert len(res.parameter) == T and res.in_round == in_round
 
@@ -1048,6 +1119,7 @@ def main_plugin(args: argparse.Namespace) -> int:
     ctx.prof_collect()
     ctx.prof_enable(not args.no_kernel_events)
     host_s[0] = 0.0
+    tail_s[0] = 0.0
     dyn0 = dict(algo.dyn_stats)
     ctx.dyn_prof_collect()
     torch.cuda.synchronize(device)
@@ -1076,6 +1148,39 @@ def main_plugin(args: argparse.Namespace) -> int:
         kstep_s = dyn_ms * 1e-3 / args.steps
         launch_bytes = job_bytes
         achieved = launch_bytes / kstep_s / 1e9 if kstep_s > 0 else 0.0
+    burst = None
+    if bursts > 1:
+        # one burst's clients folded by the one-launch kernel (HIP events): the fold time the
+        # burst's latency is judged against (last arrival -> result <= 1.2x of it)
+        bctx = FedAvgContext(layout, device)
+        btab = ClientTable(T)
+        for row, w in zip(views[-per_burst:], weights[-per_burst:]):
+            btab.add_client(row, [w] * T)
+        offs_b, pad_b = layout.padded_offsets(out_b)
+        bflat = torch.empty(pad_b, dtype=out_dtype, device=device)
+        bouts = OutputTable([bflat[o : o + n] for o, n in zip(offs_b, layout.numels)], layout, device, out_dtype)
+        bplan = bctx.plan(btab, in_dtype, bouts, out_dtype)
+        for _ in range(3):
+            bplan.run()
+        bctx.raise_on_nan()
+        bctx.prof_collect()
+        bctx.prof_enable(True)
+        for _ in range(10):
+            bplan.run()
+        bctx.raise_on_nan()
+        bctx.prof_enable(False)
+        b_ms, b_n = bctx.prof_collect()
+        del bplan
+        bctx.close()
+        burst_ms = b_ms / max(b_n, 1)
+        lat_ms = tail_s[0] / args.steps * 1e3
+        burst = {"bursts": bursts, "updates_per_burst": per_burst, "gap_ms": gap_s * 1e3,
+                 "last_arrival_to_result_ms": round(lat_ms, 4),
+                 "one_burst_fold_ms": round(burst_ms, 4),
+                 "ratio": round(lat_ms / burst_ms, 3) if burst_ms else None,
+                 "what": "last process_worker_data returned -> aggregate_worker_data returned (result on the "
+                         "device, NaN flags read), against one burst's clients folded and divided by the "
+                         "one-launch kernel (fedavg_tile_kernel, HIP events)"}
     cpu = None
     if not args.no_cpu_baseline:
         del params, views, buckets
@@ -1087,16 +1192,21 @@ def main_plugin(args: argparse.Namespace) -> int:
     short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
     gbps = round(job_bytes / step_s / 1e9, 2)
     line = {
-        "metric": ("in-round gradient FedAvg round latency (GradientWorker cadence) through the plugin surface: "
+        "metric": ("burst-cadence FedAvg round through the plugin surface (the reference server's poll-then-sleep "
+                   "loop): last arrival to result latency" if burst else
+                   "in-round gradient FedAvg round latency (GradientWorker cadence) through the plugin surface: "
                    "FedAVGAlgorithm.process_worker_data x N + aggregate_worker_data" if in_round else
                    "aggregated GB/s (device-resident) through the plugin surface: FedAVGAlgorithm."
                    "process_worker_data x N + aggregate_worker_data"),
-        "value": round(step_s * 1e3, 4) if in_round else gbps, "unit": "ms per round" if in_round else "GB/s",
+        **({"burst_arrivals": burst} if burst else {}),
+        "value": (burst["last_arrival_to_result_ms"] if burst else round(step_s * 1e3, 4) if in_round else gbps),
+        "unit": "ms last arrival to result" if burst else "ms per round" if in_round else "GB/s",
         "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": not in_round,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": not (in_round or burst),
         "scaling": "replicas only", "vs_baseline": None, "dtype": "f64", "GBps": gbps,
         "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
         "config": {"workload": (f"{'gradient' if in_round else 'plugin'}_fedavg_{args.layout}_{short}_{N}_clients"
+                                + (f"_in_{bursts}_bursts_{gap_s * 1e3:g}ms_apart" if bursts > 1 else "")
                                 + (f"_waves_of_{wave}" if n_waves > 1 and not algo.wave_min else "")
                                 + (f"_early_waves_from_{algo.wave_min}" if algo.wave_min else "")),
                    "clients": N, "params_per_client": P, "tensors_per_client": T, "in_dtype": args.in_dtype,
@@ -1727,6 +1837,9 @@ def main_one_process_under_launcher(args: argparse.Namespace) -> int | None:
 
 
 def main() -> int:
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-baseline-child":
+        print(json.dumps(_cpu_baseline_child(json.loads(sys.argv[2]))), flush=True)
+        return 0
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -1780,6 +1893,10 @@ def main() -> int:
                          "gradient: GradientWorker's in-round rounds through the plugin, as a latency "
                          "(--clients-per-gpu default 8)")
     ap.add_argument("--pers-weights", default="float", choices=["float", "int"])
+    ap.add_argument("--arrival", default="all",
+                    help="--workload plugin / gradient: 'all' (updates back to back) or bursts:K:GAP_MS — K "
+                         "bursts with GAP_MS of host time between them (the reference server's poll-then-sleep "
+                         "cadence); the line then reports last_arrival_to_result_ms")
     ap.add_argument("--launch-timeout", type=float, default=480.0,
                     help="--gpus N > 1 without an external launcher: seconds before the spawned ranks are "
                          "stopped and the run fails (one --comm torch rerun within the same budget)")

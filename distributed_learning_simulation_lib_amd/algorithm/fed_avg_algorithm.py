@@ -35,7 +35,6 @@ Differences a caller can observe, all documented in DESIGN.md:
 
 from __future__ import annotations
 
-import os
 from collections.abc import MutableMapping, Sequence
 from typing import Any
 
@@ -58,6 +57,7 @@ from ..message import (
     wire_class,
 )
 from ..quantized import QuantizedTensor, dequantize_tensor, record_layout
+from .dynamic_wave import DynamicWave, PluginSettings
 from .aggregation_algorithm import (
     AggregationAlgorithm,
     default_device,
@@ -70,9 +70,6 @@ from .aggregation_algorithm import (
 _KERNEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
 _STAGING_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # staging_ext.cpp codes
 _STAGING_CODES = {dt: code for code, dt in enumerate(_STAGING_DTYPES)}
-_DYN_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)  # dyn_wave_kernel inputs
-# host QSGD records packed by pointer (FEDAVG_QSGD_HOST_PTRS=0: through per-record views, A/B knob)
-_HOST_RECORD_PTRS = os.environ.get("FEDAVG_QSGD_HOST_PTRS", "1") != "0"
 # what a device entry of the multi-device mode keeps for itself (the rest of the round's state —
 # layout, per-name totals, flags — is one for the whole round)
 _LANE_ATTRS = ("_device", "_FedAVGAlgorithm__table", "_FedAVGAlgorithm__table_dtype",
@@ -130,55 +127,40 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         exchange: str = "peer",
         wave_min: int | None = None,
         dynamic_wave: bool | None = None,
+        settings: PluginSettings | None = None,
     ) -> None:
         super().__init__()
         self.accumulate: bool = True
         self.aggregate_loss: bool = False
         self._device = torch.device(device) if device is not None else None
+        # the tuning knobs: one settings object (PluginSettings.from_env() unless given), single
+        # fields overridden by the keyword arguments
+        self.settings = (settings or PluginSettings.from_env()).with_overrides(
+            wave_size=wave_size or None, wave_min=wave_min, eager_nan_check=eager_nan_check, dynamic_wave=dynamic_wave)
         # 64: with an update staged in ~2.6 us, folding half a 64-client round early no longer
         # pays for the extra wave's fp64 accumulator round trip and launch ramp (0.756 vs 0.789 ms
         # per device-resident 64 x ResNet-18 round; 32 was faster while
         # staging took ~4 us per update)
-        self.wave_size = int(wave_size or os.environ.get("FEDAVG_WAVE_SIZE", 64))
-        assert self.wave_size >= 1
+        self.wave_size = self.settings.wave_size
         # early waves: a wave of at least ``wave_min`` staged clients is also folded when the next
         # update arrives while the GPU has finished every wave so far (0 = only full waves), so the
         # fold starts after the first few arrivals instead of after ``wave_size`` of them
-        self.wave_min = int(os.environ.get("FEDAVG_WAVE_MIN", 0) if wave_min is None else wave_min)
-        assert self.wave_min >= 0
+        self.wave_min = self.settings.wave_min
         self.__wave_event: torch.cuda.Event | None = None  # recorded after each flushed wave
-        # The round's first wave as a dynamic wave (include/fedavg_hip.h fedavg_dyn_*): launched at
-        # the round's first staged update, handed the staged rows every FEDAVG_DYN_BATCH arrivals
-        # while it folds the ones it has, closed by the wave's flush or by aggregate_worker_data
-        # (which then divides in the same kernel) — the GPU works through the arrival phase instead
-        # of after it. Any update it cannot take (an absent tensor, per-tensor weights, unaligned
-        # tensors) or a current stream with unfinished work closes it early: it keeps the rows it
+        # The round's first wave as a dynamic wave (algorithm/dynamic_wave.py): launched at the
+        # round's first staged update, handed the staged rows while it folds the ones it has, closed
+        # by the wave's flush or by aggregate_worker_data (which then divides in the same kernel) —
+        # the GPU works through the arrival phase instead of after it. Any update it cannot take (an
+        # absent tensor, per-tensor weights, unaligned tensors) closes it early: it keeps the rows it
         # folded and the ordinary waves fold the rest, with the same bits.
-        self.dynamic_wave = (os.environ.get("FEDAVG_DYN", "1") != "0") if dynamic_wave is None else bool(dynamic_wave)
-        self.__dyn_batch = max(1, int(os.environ.get("FEDAVG_DYN_BATCH", 2)))
-        self.__dyn_table: Any = None         # the table the open dynamic wave reads
-        self.__dyn_pub = 0                   # its rows published so far
-        self.__dyn_closed: Any = None        # (table, rows folded) of the round's closed dynamic wave
-        self.__dyn_round = False             # the round's first wave has been decided
-        # rounds of fewer updates than this (the previous round's count) skip the dynamic wave: its
-        # open / close cost more than the arrivals it hides
-        self.dyn_min_rows = int(os.environ.get("FEDAVG_DYN_MIN_ROWS", 4))
-        self.__prev_arrivals: int | None = None  # the previous round's process_worker_data calls
-        # the input dtype of the last round's wave: the next round opens its wave with it before
-        # staging its first update (bound to that update's row, or closed empty if it differs)
-        self.__dyn_last: Any = None
-        self.__dyn_pre: Any = None           # the dtype of a wave opened before its first row
-        self.__dyn_pre_ctx: Any = None       # ... and the context it was opened on
+        self.__dyn = DynamicWave(self.settings.dynamic)
         self.__round_updates = 0
-        # dynamic waves opened, rows they folded, waves that wrote the round's result themselves
-        self.dyn_stats = {"waves": 0, "rows": 0, "finalized": 0}
         self.result_dtype = result_dtype
         self.result_device = torch.device(result_device) if result_device is not None else None
         self.split_policy = split_policy
         # the reference asserts each arriving tensor is NaN-free (fed_avg_algorithm.py:34-35);
         # by default the fused flags report it at the wave flush, eagerly on request
-        self.eager_nan_check = (os.environ.get("FEDAVG_EAGER_NAN") == "1") if eager_nan_check is None \
-            else bool(eager_nan_check)
+        self.eager_nan_check = self.settings.eager_nan_check
         self.__layout: ModelLayout | None = None
         self.__native_layout: ModelLayout | None = None
         self.__keep: list[int] = []
@@ -241,6 +223,22 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 lane["_device"] = d
 
     # ---- setup -------------------------------------------------------------------------
+    @property
+    def dynamic_wave(self) -> bool:
+        return self.__dyn.settings.enabled
+
+    @dynamic_wave.setter
+    def dynamic_wave(self, on: bool) -> None:
+        from dataclasses import replace
+
+        self.__dyn.settings = replace(self.__dyn.settings, enabled=bool(on))
+
+    @property
+    def dyn_stats(self) -> dict[str, int]:
+        """Dynamic waves opened, rows they folded, waves that wrote the round's result, continued
+        launches after a wave ended itself, opens the library refused (DynamicWave.stats)."""
+        return self.__dyn.stats
+
     @property
     def device(self) -> torch.device:
         if self._device is None:
@@ -390,8 +388,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_data: Message | None,
     ) -> bool:
         self.__round_updates += 1
-        if self.__round_updates == 1 and self.__dyn_last is not None:
-            self._dyn_preopen()
+        if self.__round_updates == 1:
+            self.__dyn.preopen(self._context, self._dyn_eligible(), self.__table is not None, self.wave_size)
         if worker_data is not None and self._arrive_quick(worker_id, worker_data):
             return True
         res = super().process_worker_data(worker_id, worker_data)
@@ -570,7 +568,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                     self.__table_delta = delta
                 self.__ew = False
                 self.__has_data = True
-                self._dyn_arrival()
+                self._dyn_arrival(next(iter(params.values()), None))
                 return True
         first = next(iter(params.values()), None)
         host = isinstance(first, torch.Tensor) and first.device.type == "cpu"
@@ -599,6 +597,14 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self.__table_delta = delta
         self.__table.add_resident_client(ptrs, weights, nums, dt.itemsize, dev_idx, keep)
         self.__has_data = True
+        if host:
+            # host rows: the round is PCIe-bound (the fold hides behind the DMAs), so no wave holds
+            # the GPU for it — nor, pre-opened, for the next round
+            self.__dyn.not_this_round()
+        elif type(self.__table) is NativeClientTable:
+            self._dyn_arrival(keep[0] if keep else None)
+        else:
+            self.__dyn.not_this_round()
         return True
 
     def _fast_maps(self) -> tuple | None:
@@ -786,7 +792,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 # quantised update: the records are the kernel operands (dequantised in the fold)
                 dt = codecs.pop()
                 recs = [None if t is None else t.record for t in tensors]
-                if _HOST_RECORD_PTRS and not self.eager_nan_check and \
+                if self.settings.qsgd_host_pointers and not self.eager_nan_check and \
                         all(r is None or (r.device.type == "cpu" and r.is_contiguous()) for r in recs):
                     # host records: packed from their pointers, one DMA, row pointers from the
                     # bucket offsets (no per-record views, no second per-record pass)
@@ -823,10 +829,10 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         else:
             self.__table.add_client(tensors, weights, weight_tensors if self.__ew else None)
         self.__has_data = True
-        if type(self.__table) is NativeClientTable:
-            self._dyn_arrival()
+        if resident and type(self.__table) is NativeClientTable:
+            self._dyn_arrival(keep[0] if keep else None)
         else:
-            self._dyn_unpre()
+            self.__dyn.not_this_round()  # host / converted rows, quantised records, per-element weights
 
     def _scan_arrival(self, tensors: list, dt: Any, worker_id: int | None, delta: bool) -> None:
         """fed_avg_algorithm.py:34-35 at the arrival: one GPU scan of the staged update."""
@@ -933,108 +939,44 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         ev = self.__wave_event
         return ev is None or ev.query()
 
-    # ---- the dynamic wave (fedavg_dyn_*) ------------------------------------------------
-    def _dyn_preopen(self) -> None:
-        """The round's first update is arriving: open the wave with the last round's input dtype
-        now, so the launch overlaps this update's staging (its row binds it in _dyn_arrival)."""
-        if not (self.dynamic_wave and self.device.type == "cuda" and self.__multi_devices is None
-                and self.accumulate and self.__default_hooks and not self.wave_min and not self.eager_nan_check
-                and self.__table is None and not self.__dyn_round and self.__dyn_table is None
-                and (self.__prev_arrivals is None or self.__prev_arrivals >= self.dyn_min_rows)):
-            return
-        ctx = self._context()
-        try:
-            ctx.dyn_open(self.__dyn_last, self.wave_size)
-        except _native.NativeError:
-            return
-        self.__dyn_pre, self.__dyn_pre_ctx = self.__dyn_last, ctx
+    # ---- the dynamic wave (algorithm/dynamic_wave.py) -----------------------------------
+    def _dyn_eligible(self) -> bool:
+        """The round may fold through a dynamic wave (one device, the default hooks, no early
+        waves or eager scans, scalar weights, full updates)."""
+        return (self.dynamic_wave and self.device.type == "cuda" and self.__multi_devices is None and self.accumulate
+                and self.__default_hooks and not self.wave_min and not self.eager_nan_check
+                and self.__ew is not True and not self.__table_delta and self.__native_layout is not None)
 
-    def _dyn_unpre(self) -> None:
-        """Close a wave opened before its first row that no row will bind (it folded nothing)."""
-        if self.__dyn_pre is not None:
-            ctx, self.__dyn_pre, self.__dyn_pre_ctx = self.__dyn_pre_ctx, None, None
-            try:
-                ctx.dyn_close(None)
-            except _native.NativeError:
-                pass  # its context was replaced (a grown layout): closing it ended the wave
+    def _dyn_arrival(self, probe: Any = None) -> None:
+        """A device-resident row joined the table (``probe``: one of its tensors, checked at the
+        round's first row only)."""
+        dyn = self.__dyn
+        if dyn.table is not None:
+            dyn.more(self.__table)  # the common arrival: at most one publication
+        elif not dyn.decided:
+            dyn.arrival(self.__table, self._context,
+                        self._dyn_eligible() and self.__ew is False and not self._shared_device(probe),
+                        self.__table_dtype, self.wave_size)
 
-    def _dyn_arrival(self) -> None:
-        """A row joined the wave's native table: open the round's dynamic wave at the first one
-        (when the round qualifies), then hand it the staged rows every ``FEDAVG_DYN_BATCH``."""
-        table = self.__table
-        if self.__dyn_table is None:
-            if self.__dyn_round:
-                return
-            self.__dyn_round = True
-            if not (self.dynamic_wave and type(table) is NativeClientTable and table.num_clients == 1
-                    and self.device.type == "cuda"
-                    and self.__multi_devices is None and self.accumulate and self.__default_hooks
-                    and not self.wave_min and not self.eager_nan_check and self.__ew is False
-                    and not self.__table_delta and self.__table_dtype in _DYN_DTYPES
-                    and (self.__prev_arrivals is None or self.__prev_arrivals >= self.dyn_min_rows)):
-                self._dyn_unpre()
-                self.__dyn_last = None
-                return
-            if self.__dyn_pre is not None and (self.__dyn_pre != self.__table_dtype
-                                               or self.__dyn_pre_ctx is not self._context()):
-                self._dyn_unpre()  # opened for another dtype or context: reopen for this one
-            if self.__dyn_pre is None:
-                try:
-                    self._context().dyn_open(self.__table_dtype, self.wave_size)
-                except _native.NativeError:
-                    return  # e.g. the accumulator already holds data: the ordinary waves
-            self.__dyn_pre = self.__dyn_pre_ctx = None
-            self.__dyn_last = self.__table_dtype
-            self.__dyn_table, self.__dyn_pub, self.__dyn_closed = table, 0, None
-            self.dyn_stats["waves"] += 1
-        elif self.__dyn_table is not table:
-            return
-        if table.num_clients - self.__dyn_pub >= self.__dyn_batch or self.__dyn_pub == 0:
-            self._dyn_publish()  # (the first row at once: the wave starts folding)
-
-    def _dyn_publish(self) -> None:
-        """Every staged row of the dynamic wave's table to the wave (none while the current stream
-        has unfinished work); a row it cannot take closes it with the rows it has."""
-        try:
-            self.__dyn_pub += self._context().dyn_publish(self.__dyn_table)
-        except _native.NativeError as e:
-            self.__dyn_pub += getattr(e, "published", 0)
-            self._dyn_close(None)
-
-    def _dyn_close(self, outs: Any, out_dtype: torch.dtype = torch.float64, join: bool = True) -> bool:
-        """Close the open dynamic wave: into ``outs`` (True: the round's result is written) or into
-        the accumulator (the rows it folded; ``_dyn_rest`` gives the ordinary calls the rest)."""
-        table = self.__dyn_table
-        self.__dyn_table = None
-        folded, finalized = self._context().dyn_close(outs, out_dtype, join)
-        self.__dyn_closed = (table, folded)
-        self.dyn_stats["rows"] += folded
-        self.dyn_stats["finalized"] += int(finalized)
-        return finalized
-
-    def _dyn_rest(self, table: Any) -> Any:
-        """The part of ``table`` the ordinary calls fold: all of it, its rows after those a closed
-        dynamic wave folded (``TableTail``), or None when the wave folded every row."""
-        closed = self.__dyn_closed
-        if closed is None or closed[0] is not table or not closed[1]:
-            return table
-        self.__dyn_closed = None
-        return TableTail(table, closed[1]) if closed[1] < table.num_clients else None
+    @staticmethod
+    def _shared_device(t: Any) -> bool:
+        """The row's memory came from another process (CUDA IPC from a worker — which then holds a
+        context on this GPU and computes there — or external memory): the wave stays off for the
+        round, since its workgroups hold the register file while they wait for rows."""
+        ext = _staging.module()
+        return isinstance(t, torch.Tensor) and ext is not None and bool(ext.foreign(t))
 
     def _flush(self) -> None:
         """Fold the staged wave into the device accumulator (one kernel launch)."""
-        self._dyn_unpre()
+        self.__dyn.unpre()
         if self.__table is None or self.__table.num_clients == 0:
             return
         ctx = self._context()
         table, dt = self.__table, self.__table_dtype
         assert dt is not None
         self.__table, self.__table_dtype = None, None
-        if self.__dyn_table is table:  # a full dynamic wave: its rows stay in the accumulator
-            self._dyn_publish()
-            if self.__dyn_table is table:
-                self._dyn_close(None)
-        table = self._dyn_rest(table)
+        self.__dyn.flush(table)  # a full dynamic wave: its rows stay in the accumulator
+        table = self.__dyn.rest(table)
         if table is None:
             return
         if self.__ew:
@@ -1081,18 +1023,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return out
 
     def _reset_round(self) -> None:
-        try:
-            self._dyn_unpre()
-        except _native.NativeError:
-            self.__dyn_pre = None
-        if self.__dyn_table is not None:  # an abandoned round's dynamic wave ends with its rows
-            try:
-                self._dyn_close(None)
-            except _native.NativeError:
-                pass
-        self.__dyn_closed, self.__dyn_round = None, False
-        if self.__round_updates:
-            self.__prev_arrivals = self.__round_updates
+        self.__dyn.end_round(self.__round_updates)  # an abandoned round's wave ends with its rows
         self.__round_updates = 0
         self.__arrivals = 0
         self.__has_data = False
@@ -1123,9 +1054,9 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return moved
 
     def _finish_native(self) -> ModelParameter:
-        self._dyn_unpre()
-        if self.__dyn_table is not None and self.__dyn_table is self.__table:
-            self._dyn_publish()  # the last rows to the wave first: it folds them while the result is prepared
+        self.__dyn.unpre()
+        if self.__dyn.table is not None and self.__dyn.table is self.__table:
+            self.__dyn.publish()  # the last rows to the wave first: it folds them while the result is prepared
         if self.__multi_devices is not None:
             if not self.__ew:
                 return self._finish_multi()
@@ -1150,20 +1081,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         flat, outs, views = self._result_buffer(out_dtype, reuse=not custom_divide)
         self.__result_flat = None if custom_divide else flat
         delta = self.__table_delta and table is not None
-        done = False  # the dynamic wave wrote the result
-        if table is not None and self.__dyn_table is table and self.__dyn_pub < table.num_clients:
-            # the last arrivals' copies / conversions were still running at the first publication:
-            # wait for them, as the one-launch path would, so the wave can take every row
-            torch.cuda.current_stream(self.device).synchronize()
-            self._dyn_publish()  # (a row it cannot take closes the wave here: the rest below)
-        if table is not None and self.__dyn_table is table and self.__dyn_pub < table.num_clients:
-            self._dyn_close(None)  # rows left unpublished: the wave keeps its rows, the rest below
-        if table is not None and self.__dyn_table is table:
-            # join=False: raise_on_nan below waits for the wave before anything reads the outputs
-            done = self._dyn_close(None if (self.__ew or custom_divide or host_divide or delta) else outs, out_dtype,
-                                   join=False)
+        # the dynamic wave wrote the result (else its rows are in the accumulator: the rest below)
+        done = self.__dyn.finish(table, None if (self.__ew or custom_divide or host_divide or delta) else outs,
+                                 out_dtype, torch.cuda.current_stream(self.device)) if table is not None else False
         if not done and table is not None:
-            table = self._dyn_rest(table)
+            table = self.__dyn.rest(table)
         try:
             if done:
                 pass

@@ -917,10 +917,12 @@ struct DynArgs {
   double* wtot;
   uint64_t* outs;
   DynMirror* mir;
+  uint32_t* elect;          // the mirror election word (device memory): the wave's epoch once taken
   int32_t num_tiles;
   int32_t num_segs;
   int32_t cap;
   uint32_t epoch;
+  int32_t resume;           // 1: the accumulators start from the fp64 accumulator (a continued wave)
   uint64_t idle_ticks;      // s_memrealtime ticks (100 MHz)
   uint64_t life_ticks;
 };
@@ -935,6 +937,29 @@ __device__ __forceinline__ void dyn_st_sys64(uint64_t* p, uint64_t v) {
 }
 __device__ __forceinline__ double dyn_ld_sysf(const double* p) {
   return __longlong_as_double(static_cast<long long>(dyn_ld_sys64(reinterpret_cast<const uint64_t*>(p))));
+}
+
+// The mirror role goes to the first leading workgroup to arrive: each launch of the wave (body and
+// edge, on two streams) starts with one candidate workgroup, the loser leaves at once. A launch's
+// leading workgroup is dispatched before the rest of it, so whichever launch holds CU slots also
+// holds (or held) the mirror, and no tile can spin on a mirror that waits for those slots. Were
+// that ordering ever broken, the tiles' own lifetime bound still ends the wave (ack->error).
+__device__ bool dyn_elect(const DynArgs& a) {
+  __shared__ int32_t s_win;
+  if (threadIdx.x == 0) {
+    uint32_t cur = __hip_atomic_load(a.elect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t win = 0;
+    while (cur != a.epoch) {
+      if (__hip_atomic_compare_exchange_strong(a.elect, &cur, a.epoch, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        win = 1;
+        break;
+      }
+    }
+    s_win = win;
+  }
+  __syncthreads();
+  return s_win != 0;
 }
 
 __device__ void dyn_mirror(const DynArgs& a) {
@@ -1111,8 +1136,8 @@ __device__ __forceinline__ void dyn_prime(DynV<T> (&buf)[NB], gptr<const DynV<T>
 template <typename T, bool EDGE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kDynLanes, kDynLanes), amdgpu_waves_per_eu(2, 8)))
 void dyn_wave_kernel(DynArgs a) {
-  if (!EDGE && blockIdx.x == 0) {
-    dyn_mirror(a);
+  if (blockIdx.x == 0) {  // the launch's mirror candidate
+    if (dyn_elect(a)) dyn_mirror(a);
     return;
   }
   constexpr int AE = EDGE ? kDynAEEdge : kDynAE;
@@ -1134,20 +1159,37 @@ void dyn_wave_kernel(DynArgs a) {
 
   __shared__ double s_tail[N];
 
-  const TileDesc td = load_tile(EDGE ? a.edge_tiles : a.tiles, blockIdx.x - (EDGE ? 0 : 1));
+  const TileDesc td = load_tile(EDGE ? a.edge_tiles : a.tiles, blockIdx.x - 1);
   const int seg = td.seg;
   const int count = td.count;
   const bool full = !EDGE;  // body tiles are whole (count == TILE)
   const int nfull = count / N;        // whole 16-B vectors of the tile
   const int tail = count - nfull * N; // elements past them (a segment's last tile)
   const int li = static_cast<int>(threadIdx.x);
-  if (li < N) s_tail[li] = -0.0;
   const int64_t elem_off = td.start * static_cast<int64_t>(sizeof(T));
   const int64_t acc_base = to_const<int64_t>(a.segs)[2 * seg] + td.start;  // SegDesc::acc_off
+  const gptr<const double> acc_in = to_global<double>(a.acc + acc_base);
+  if (li < N) s_tail[li] = (a.resume && li < tail) ? acc_in[static_cast<int64_t>(nfull) * N + li] : -0.0;
 
   double acc[AE];  // element (v * 64 + li) * N + q of the tile at acc[v * N + q]
 #pragma unroll
   for (int i = 0; i < AE; ++i) acc[i] = -0.0;  // the additive identity (see tile_body)
+  if (a.resume) {
+    // a continued wave: the rows earlier waves of the round folded, from the fp64 accumulator the
+    // previous wave's accumulator close stored (the same element order as the close below)
+#pragma unroll
+    for (int v = 0; v < AE / N; ++v) {
+      if (full || v * kDynLanes + li < nfull) {
+        const gptr<const f64x2> src = reinterpret_cast<gptr<const f64x2>>(acc_in + static_cast<int64_t>(v * kDynLanes + li) * N);
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) {
+          const f64x2 x = src[q];
+          acc[v * N + 2 * q] = x.x;
+          acc[v * N + 2 * q + 1] = x.y;
+        }
+      }
+    }
+  }
   (void)TILE;
 
   const DynMirror* const mir = a.mir + (blockIdx.x % kDynCopies);
@@ -2203,6 +2245,12 @@ struct fedavg_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t start = nullptr, done = nullptr;
     std::vector<double> wsum;  // per segment, the published rows' weights in arrival order
+    // a wave that ended itself is continued by a fresh launch (dyn_continue): rows [0, base) of the
+    // caller's table are in the accumulator, wsum_base their per-segment totals in arrival order
+    int32_t base = 0;
+    std::vector<double> wsum_base;
+    int32_t reopens = 0;   // continued waves, cumulative (fedavg_dyn_info)
+    int32_t launches = 0;  // wave launches, cumulative
     uint64_t idle_ticks = 0, life_ticks = 0;
   } dyn;
 };
@@ -3122,7 +3170,8 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
     // an open dynamic wave ends with the rows it has (its ACK arrives within a mirror poll)
     const DynLayout L(c->T, c->dyn.cap);
     DynCtl* ctl = reinterpret_cast<DynCtl*>(c->dyn.host + L.ctl);
-    __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(c->dyn.published), 1u, OUT_ACC, 0u), __ATOMIC_RELEASE);
+    __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(c->dyn.published - c->dyn.base), 1u, OUT_ACC, 0u),
+                     __ATOMIC_RELEASE);
     c->dyn.active = false;
   }
   if (c->dyn.stream) (void)hipStreamSynchronize(c->dyn.stream);
@@ -4094,12 +4143,13 @@ struct DynTrace {
 };
 
 int32_t dyn_wait_ack(fedavg_ctx* c, uint32_t* state, uint32_t* count) {
-  const DynLayout L(c->T, c->dyn.cap);
-  const DynAck* ack = reinterpret_cast<const DynAck*>(c->dyn.host + L.ack);
+  auto& d = c->dyn;
+  const DynLayout L(c->T, d.cap);
+  const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
   // the mirror answers within a poll (~1 µs); a wave whose mirror never runs is ended by its
   // own lifetime limit, so this wait is bounded by that (plus a margin)
   const auto t0 = std::chrono::steady_clock::now();
-  const double limit_s = static_cast<double>(c->dyn.life_ticks) / 1e8 + 5.0;
+  const double limit_s = static_cast<double>(d.life_ticks) / 1e8 + 5.0;
   for (;;) {
     const uint64_t aw = __atomic_load_n(&ack->word, __ATOMIC_ACQUIRE);
     const uint32_t st = static_cast<uint32_t>(aw);
@@ -4108,12 +4158,138 @@ int32_t dyn_wait_ack(fedavg_ctx* c, uint32_t* state, uint32_t* count) {
       *count = static_cast<uint32_t>(aw >> 32);
       return FEDAVG_OK;
     }
-    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
-      return fail(FEDAVG_ERR_HIP, "the dynamic wave did not acknowledge its close");
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+      // the context recovers: the wave is no longer open, the accumulator holds nothing valid, and
+      // the next open waits for the wave's launches (their tiles end themselves after life + 1 s)
+      d.active = false;
+      d.unjoined = false;
+      std::fill(c->valid.begin(), c->valid.end(), 0);
+      (void)hipEventRecord(d.done, d.stream);
+      if (!d.edge_tiles.empty()) (void)hipEventRecord(d.edge_done, d.edge_stream);
+      return fail(FEDAVG_ERR_HIP, "the dynamic wave did not acknowledge its close (the wave is abandoned)");
+    }
 #if defined(__x86_64__)
     __builtin_ia32_pause();
 #endif
   }
+}
+
+// The wave's two launches on the private streams: the body tiles, then the edge tiles, each led by
+// a mirror candidate workgroup (dyn_elect). `resume`: the accumulators start from the fp64
+// accumulator (a wave continuing the round after an earlier one ended itself).
+int32_t dyn_launch(fedavg_ctx* c, int32_t resume) {
+  auto& d = c->dyn;
+  const DynLayout L(c->T, d.cap);
+  d.epoch = g_dyn_epoch.fetch_add(1) + 1;
+  if (d.epoch == 0) d.epoch = g_dyn_epoch.fetch_add(1) + 1;
+  DynArgs a{};
+  a.tiles = d.d_tiles;
+  a.edge_tiles = d.d_edge_tiles;
+  a.segs = c->d_segs;
+  a.acc = c->acc;
+  a.flag = c->d_flag;
+  a.ctl = reinterpret_cast<DynCtl*>(d.dev_alias + L.ctl);
+  a.ack = reinterpret_cast<DynAck*>(d.dev_alias + L.ack);
+  a.h_wtot = reinterpret_cast<const double*>(d.dev_alias + L.wtot);
+  a.h_outs = reinterpret_cast<const uint64_t*>(d.dev_alias + L.outs);
+  a.h_wtab = reinterpret_cast<const double*>(d.dev_alias + L.wtab);
+  a.h_ptab = reinterpret_cast<const uint64_t*>(d.dev_alias + L.ptab);
+  a.wtot = reinterpret_cast<double*>(d.dtab + L.wtot);
+  a.outs = reinterpret_cast<uint64_t*>(d.dtab + L.outs);
+  a.wtab = reinterpret_cast<double*>(d.dtab + L.wtab);
+  a.ptab = reinterpret_cast<uint64_t*>(d.dtab + L.ptab);
+  a.mir = reinterpret_cast<DynMirror*>(d.mirror);
+  a.elect = reinterpret_cast<uint32_t*>(d.mirror + sizeof(DynMirror) * kDynCopies);
+  a.num_tiles = static_cast<int32_t>(d.tiles.size());
+  a.num_segs = c->T;
+  a.cap = d.cap;
+  a.epoch = d.epoch;
+  a.idle_ticks = d.idle_ticks;
+  a.life_ticks = d.life_ticks;
+  a.resume = resume;
+  d.prof_start = nullptr;
+  if (c->prof) {  // the body launch timed from its enqueue to its end (arrivals included)
+    d.prof_start = take_event(c);
+    if (!d.prof_start) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
+    FEDAVG_HIP_TRY(hipEventRecord(d.prof_start, d.stream));
+  }
+  const dim3 grid(static_cast<unsigned>(a.num_tiles + 1)), block(kDynLanes);
+  switch (d.in_dtype) {
+    case FEDAVG_F32: hipLaunchKernelGGL((dyn_wave_kernel<float, false>), grid, block, 0, d.stream, a); break;
+    case FEDAVG_F16: hipLaunchKernelGGL((dyn_wave_kernel<__half, false>), grid, block, 0, d.stream, a); break;
+    case FEDAVG_BF16: hipLaunchKernelGGL((dyn_wave_kernel<bf16_t, false>), grid, block, 0, d.stream, a); break;
+    default: hipLaunchKernelGGL((dyn_wave_kernel<double, false>), grid, block, 0, d.stream, a); break;
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  if (!d.edge_tiles.empty()) {
+    const dim3 egrid(static_cast<unsigned>(d.edge_tiles.size() + 1));
+    switch (d.in_dtype) {
+      case FEDAVG_F32: hipLaunchKernelGGL((dyn_wave_kernel<float, true>), egrid, block, 0, d.edge_stream, a); break;
+      case FEDAVG_F16: hipLaunchKernelGGL((dyn_wave_kernel<__half, true>), egrid, block, 0, d.edge_stream, a); break;
+      case FEDAVG_BF16: hipLaunchKernelGGL((dyn_wave_kernel<bf16_t, true>), egrid, block, 0, d.edge_stream, a); break;
+      default: hipLaunchKernelGGL((dyn_wave_kernel<double, true>), egrid, block, 0, d.edge_stream, a); break;
+    }
+  }
+  FEDAVG_HIP_TRY(hipGetLastError());
+  ++d.launches;
+  return FEDAVG_OK;
+}
+
+// The open wave ended itself (FEDAVG_DYN_IDLE_US without a row, or FEDAVG_DYN_LIFE_US): its
+// accumulator close stored rows [base, base + folded). A fresh wave continues the round from that
+// accumulator — the reference server's poll loop (server.py:133-146) hands updates over in bursts
+// with a sleep between them, and a burst after the idle limit is folded while it arrives instead
+// of in one launch at aggregate_worker_data. Rows published to the ended wave after it stopped
+// reading are moved to the front of the new wave's table.
+int32_t dyn_continue(fedavg_ctx* c) {
+  auto& d = c->dyn;
+  DynTrace tr("reopen");
+  const int T = c->T;
+  const DynLayout L(T, d.cap);
+  DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
+  DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);
+  const uint64_t aw = __atomic_load_n(&ack->word, __ATOMIC_ACQUIRE);
+  const int32_t folded = static_cast<int32_t>(aw >> 32);
+  FEDAVG_HIP_TRY(hipSetDevice(c->device));
+  // the ended wave's launches read the device table and write the accumulator: both finished
+  // before the next mirror rewrites the table and the next tiles read the accumulator (the usual
+  // case — the burst comes after the idle limit — finds them long done)
+  FEDAVG_HIP_TRY(hipEventRecord(d.done, d.stream));
+  if (!d.edge_tiles.empty()) FEDAVG_HIP_TRY(hipEventRecord(d.edge_done, d.edge_stream));
+  if (hipEventQuery(d.done) != hipSuccess) FEDAVG_HIP_TRY(hipEventSynchronize(d.done));
+  if (!d.edge_tiles.empty() && hipEventQuery(d.edge_done) != hipSuccess) FEDAVG_HIP_TRY(hipEventSynchronize(d.edge_done));
+  tr.mark("prev");
+  if (__atomic_load_n(&ack->error, __ATOMIC_ACQUIRE)) {
+    d.active = false;
+    std::fill(c->valid.begin(), c->valid.end(), 0);
+    return fail(FEDAVG_ERR_HIP, "a dynamic wave's workgroup lost its mirror (the wave's results are invalid)");
+  }
+  if (d.prof_start) {
+    hipEvent_t stop = take_event(c);
+    if (!stop) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
+    FEDAVG_HIP_TRY(hipEventRecord(stop, d.stream));
+    d.prof.emplace_back(d.prof_start, stop);
+    d.prof_start = nullptr;
+  }
+  double* wtab = reinterpret_cast<double*>(d.host + L.wtab);
+  uint64_t* ptab = reinterpret_cast<uint64_t*>(d.host + L.ptab);
+  for (int t = 0; t < T; ++t)
+    for (int32_t k = 0; k < folded; ++k) d.wsum_base[t] += wtab[k];  // fed_avg_algorithm.py:59-62, arrival order
+  const int32_t left = d.published - d.base - folded;
+  if (left > 0 && folded > 0) {
+    std::memmove(wtab, wtab + folded, sizeof(double) * left);
+    for (int t = 0; t < T; ++t)
+      std::memmove(ptab + static_cast<int64_t>(t) * d.cap, ptab + static_cast<int64_t>(t) * d.cap + folded,
+                   sizeof(uint64_t) * left);
+  }
+  d.base += folded;
+  __atomic_store_n(&ack->word, uint64_t{0}, __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->error, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(left), 0u, OUT_ACC, 0u), __ATOMIC_RELEASE);
+  ++d.reopens;
+  tr.mark("table");
+  // nothing folded yet (a wave opened ahead of its first row that idled out): a zero-initialised wave
+  return dyn_launch(c, d.base > 0 ? 1 : 0);
 }
 
 }  // namespace
@@ -4137,11 +4313,13 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.edge_done, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.start, hipEventDisableTiming));
     FEDAVG_HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
-    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.mirror), sizeof(DynMirror) * kDynCopies));
+    // kDynCopies mirror words, then the election word (dyn_elect)
+    const size_t mbytes = sizeof(DynMirror) * (kDynCopies + 1);
+    FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.mirror), mbytes));
     // epoch 0 is never a wave's; on the wave's own stream and waited for: a plain hipMemset
     // is not ordered before a launch on a non-blocking stream, and a recycled allocation may
     // hold another context's mirror words (epochs are process-wide besides: g_dyn_epoch)
-    FEDAVG_HIP_TRY(hipMemsetAsync(d.mirror, 0, sizeof(DynMirror) * kDynCopies, d.stream));
+    FEDAVG_HIP_TRY(hipMemsetAsync(d.mirror, 0, mbytes, d.stream));
     FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
     for (int t = 0; t < c->T; ++t) {  // body tiles, then each segment's rest as edge tiles
       const int64_t n = c->seg_numel[t], body = n / kDynTile * kDynTile;
@@ -4154,8 +4332,8 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
       FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(dev), sizeof(TileDesc) * host->size()));
       FEDAVG_HIP_TRY(hipMemcpy(*dev, host->data(), sizeof(TileDesc) * host->size(), hipMemcpyHostToDevice));
     }
-    d.idle_ticks = dyn_env_us("FEDAVG_DYN_IDLE_US", 500) * 100;      // s_memrealtime: 100 MHz
-    d.life_ticks = dyn_env_us("FEDAVG_DYN_LIFE_US", 2000000) * 100;
+    if (!d.idle_ticks) d.idle_ticks = dyn_env_us("FEDAVG_DYN_IDLE_US", 500) * 100;  // s_memrealtime: 100 MHz
+    if (!d.life_ticks) d.life_ticks = dyn_env_us("FEDAVG_DYN_LIFE_US", 2000000) * 100;
   }
   if (d.cap < max_clients) {
     FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));  // the previous wave has left the old block
@@ -4186,7 +4364,9 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   __atomic_store_n(&ack->word, uint64_t{0}, __ATOMIC_RELAXED);
   __atomic_store_n(&ack->error, 0u, __ATOMIC_RELEASE);
   d.wsum.assign(c->T, -0.0);
+  d.wsum_base.assign(c->T, -0.0);
   d.published = 0;
+  d.base = 0;
   d.in_dtype = in_dtype;
   // the wave starts behind the caller's stream (what it enqueued so far), on the private stream;
   // an idle caller's stream (the usual case: the previous round ended on the host) needs no
@@ -4200,57 +4380,8 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   } else {
     tr.mark("query");
   }
-  d.epoch = g_dyn_epoch.fetch_add(1) + 1;
-  if (d.epoch == 0) d.epoch = g_dyn_epoch.fetch_add(1) + 1;
-  DynArgs a{};
-  a.tiles = d.d_tiles;
-  a.edge_tiles = d.d_edge_tiles;
-  a.segs = c->d_segs;
-  a.acc = c->acc;
-  a.flag = c->d_flag;
-  a.ctl = reinterpret_cast<DynCtl*>(d.dev_alias + L.ctl);
-  a.ack = reinterpret_cast<DynAck*>(d.dev_alias + L.ack);
-  a.h_wtot = reinterpret_cast<const double*>(d.dev_alias + L.wtot);
-  a.h_outs = reinterpret_cast<const uint64_t*>(d.dev_alias + L.outs);
-  a.h_wtab = reinterpret_cast<const double*>(d.dev_alias + L.wtab);
-  a.h_ptab = reinterpret_cast<const uint64_t*>(d.dev_alias + L.ptab);
-  a.wtot = reinterpret_cast<double*>(d.dtab + L.wtot);
-  a.outs = reinterpret_cast<uint64_t*>(d.dtab + L.outs);
-  a.wtab = reinterpret_cast<double*>(d.dtab + L.wtab);
-  a.ptab = reinterpret_cast<uint64_t*>(d.dtab + L.ptab);
-  a.mir = reinterpret_cast<DynMirror*>(d.mirror);
-  a.num_tiles = static_cast<int32_t>(d.tiles.size());
-  a.num_segs = c->T;
-  a.cap = d.cap;
-  a.epoch = d.epoch;
-  a.idle_ticks = d.idle_ticks;
-  a.life_ticks = d.life_ticks;
-  d.prof_start = nullptr;
-  if (c->prof) {  // the body launch timed from its enqueue to its end (arrivals included)
-    d.prof_start = take_event(c);
-    if (!d.prof_start) return fail(FEDAVG_ERR_HIP, "hipEventCreate failed");
-    FEDAVG_HIP_TRY(hipEventRecord(d.prof_start, d.stream));
-  }
-  // the body launch (its workgroup 0 is the mirror) first, so its workgroups are resident first
-  const dim3 grid(static_cast<unsigned>(a.num_tiles + 1)), block(kDynLanes);
-  switch (in_dtype) {
-    case FEDAVG_F32: hipLaunchKernelGGL((dyn_wave_kernel<float, false>), grid, block, 0, d.stream, a); break;
-    case FEDAVG_F16: hipLaunchKernelGGL((dyn_wave_kernel<__half, false>), grid, block, 0, d.stream, a); break;
-    case FEDAVG_BF16: hipLaunchKernelGGL((dyn_wave_kernel<bf16_t, false>), grid, block, 0, d.stream, a); break;
-    default: hipLaunchKernelGGL((dyn_wave_kernel<double, false>), grid, block, 0, d.stream, a); break;
-  }
-  FEDAVG_HIP_TRY(hipGetLastError());
-  tr.mark("body");
-  if (!d.edge_tiles.empty()) {
-    const dim3 egrid(static_cast<unsigned>(d.edge_tiles.size()));
-    switch (in_dtype) {
-      case FEDAVG_F32: hipLaunchKernelGGL((dyn_wave_kernel<float, true>), egrid, block, 0, d.edge_stream, a); break;
-      case FEDAVG_F16: hipLaunchKernelGGL((dyn_wave_kernel<__half, true>), egrid, block, 0, d.edge_stream, a); break;
-      case FEDAVG_BF16: hipLaunchKernelGGL((dyn_wave_kernel<bf16_t, true>), egrid, block, 0, d.edge_stream, a); break;
-      default: hipLaunchKernelGGL((dyn_wave_kernel<double, true>), egrid, block, 0, d.edge_stream, a); break;
-    }
-  }
-  FEDAVG_HIP_TRY(hipGetLastError());
+  FEDAVG_RET(dyn_launch(c, 0));
+  tr.mark("launch");
   d.active = true;
   return FEDAVG_OK;
 }
@@ -4261,7 +4392,7 @@ int32_t fedavg_dyn_publish(fedavg_ctx* c, const void* const* client_ptrs, const 
   auto& d = c->dyn;
   if (published_out) *published_out = 0;
   if (!d.active) return fail(FEDAVG_ERR_STATE, "no dynamic wave is open");
-  if (K < d.published || K > d.cap) return fail(FEDAVG_ERR_INVALID, "row count outside the wave's table");
+  if (K < d.published || K - d.base > d.cap) return fail(FEDAVG_ERR_INVALID, "row count outside the wave's table");
   if (K == d.published) return FEDAVG_OK;
   const int T = c->T;
   // rows the wave can take: every tensor present, 16-B aligned, one weight per row; the rows
@@ -4282,19 +4413,23 @@ int32_t fedavg_dyn_publish(fedavg_ctx* c, const void* const* client_ptrs, const 
   // complete (the wave runs on its own stream); otherwise nothing is published now
   if (good > d.published && hipStreamQuery(static_cast<hipStream_t>(stream)) == hipSuccess) {
     const DynLayout L(T, d.cap);
+    const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
+    if (static_cast<uint32_t>(__atomic_load_n(&ack->word, __ATOMIC_ACQUIRE)) != 0)
+      FEDAVG_RET(dyn_continue(c));  // the wave ended itself: a fresh one continues the round
     uint64_t* ptab = reinterpret_cast<uint64_t*>(d.host + L.ptab);
     double* wtab = reinterpret_cast<double*>(d.host + L.wtab);
     for (int k = d.published; k < good; ++k) {
       const double w = weights[static_cast<int64_t>(k) * T];
-      wtab[k] = w;
+      const int r = k - d.base;  // the row's place in the current wave's table
+      wtab[r] = w;
       for (int t = 0; t < T; ++t) {
-        ptab[static_cast<int64_t>(t) * d.cap + k] =
+        ptab[static_cast<int64_t>(t) * d.cap + r] =
             reinterpret_cast<uint64_t>(client_ptrs[static_cast<int64_t>(k) * T + t]);
         d.wsum[t] += w;  // fed_avg_algorithm.py:59-62, arrival order
       }
     }
     DynCtl* ctl = reinterpret_cast<DynCtl*>(d.host + L.ctl);
-    __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(good), 0u, OUT_ACC, 0u), __ATOMIC_RELEASE);
+    __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(good - d.base), 0u, OUT_ACC, 0u), __ATOMIC_RELEASE);
     if (published_out) *published_out = good - d.published;
     d.published = good;
   } else if (good == K) {
@@ -4330,7 +4465,7 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
       mode = static_cast<uint32_t>(ok);
     }
   }
-  __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(d.published), 1u, mode, 0u), __ATOMIC_RELEASE);
+  __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(d.published - d.base), 1u, mode, 0u), __ATOMIC_RELEASE);
   uint32_t state = 0, folded = 0;
   tr.mark("ctl");
   FEDAVG_RET(dyn_wait_ack(c, &state, &folded));
@@ -4356,8 +4491,8 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
   tr.mark("events");
   if (tr.on) {
     const DynAck* ak = reinterpret_cast<const DynAck*>(d.host + L.ack);
-    tr.len += std::snprintf(tr.buf + tr.len, sizeof(tr.buf) - tr.len, " gpu_seen_to_ack=%.1f polls=%u",
-                            static_cast<double>(ak->t_done - ak->t_seen) / 100.0, ak->polls);
+    tr.len += std::snprintf(tr.buf + tr.len, sizeof(tr.buf) - tr.len, " gpu_seen_to_ack=%.1f polls=%u reopens=%d",
+                            static_cast<double>(ak->t_done - ak->t_seen) / 100.0, ak->polls, d.reopens);
   }
   const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
   if (__atomic_load_n(&ack->error, __ATOMIC_ACQUIRE)) {
@@ -4367,20 +4502,37 @@ int32_t fedavg_dyn_close(fedavg_ctx* c, void* const* out_ptrs, int32_t out_dtype
     return fail(FEDAVG_ERR_HIP, "a dynamic wave's workgroup lost its mirror (the wave's results are invalid)");
   }
   const bool finalized = state == 1 && mode != OUT_ACC;
+  const int32_t total = d.base + static_cast<int32_t>(folded);  // rows of the round in the accumulator
   if (finalized) {
     fedavg_internal_clear_state(c);  // the round's result is written (fed_avg_algorithm.py:90,98)
-  } else if (folded > 0) {
-    // the accumulator holds rows [0, folded): their totals, in arrival order
+  } else if (total > 0) {
+    // the accumulator holds rows [0, total): their totals, in arrival order
     const double* wtab = reinterpret_cast<const double*>(d.host + L.wtab);
     for (int t = 0; t < T; ++t) {
-      double s = -0.0;
+      double s = d.wsum_base[t];
       for (uint32_t k = 0; k < folded; ++k) s += wtab[k];
       c->wsum[t] = s;
       c->valid[t] = 1;
     }
   }
-  if (folded_out) *folded_out = static_cast<int32_t>(folded);
+  if (folded_out) *folded_out = total;
   if (finalized_out) *finalized_out = finalized ? 1 : 0;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_configure(fedavg_ctx* c, int64_t idle_us, int64_t life_us) {
+  FEDAVG_RET(check_ctx(c));
+  if (idle_us < 0 || life_us < 0) return fail(FEDAVG_ERR_INVALID, "idle / life limits must be >= 0");
+  if (idle_us) c->dyn.idle_ticks = static_cast<uint64_t>(idle_us) * 100;  // s_memrealtime: 100 MHz
+  if (life_us) c->dyn.life_ticks = static_cast<uint64_t>(life_us) * 100;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_info(const fedavg_ctx* c, int32_t* info, int32_t n) {
+  FEDAVG_RET(check_ctx(c));
+  const auto& d = c->dyn;
+  const int32_t v[5] = {d.active ? 1 : 0, d.published, d.base, d.reopens, d.launches};
+  for (int32_t i = 0; i < n && i < 5; ++i) info[i] = v[i];
   return FEDAVG_OK;
 }
 

@@ -258,6 +258,12 @@ bool allocator_owned(const at::Tensor& flat) {
   return want != nullptr && flat.storage().data_ptr().get_deleter() == want;
 }
 
+// foreign(t) — t's memory was not allocated by this process's allocator: a tensor received from
+// another process through torch.multiprocessing (CUDA IPC: the sender holds a context on this GPU,
+// e.g. a worker training there), or external memory. FedAVGAlgorithm then keeps its dynamic wave
+// off for the round (the wave would hold the register file while that process computes).
+bool foreign(const at::Tensor& t) { return t.has_storage() && t.storage().data() != nullptr && !allocator_owned(t); }
+
 bool unobserved(const at::Tensor& flat, py::list views, py::list offsets, py::list shapes) {
   const Py_ssize_t T = PyList_GET_SIZE(views.ptr());
   const ShapeSet* shp = g_shapes.get(shapes.ptr());
@@ -495,4 +501,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_pointers", &row_pointers);
   m.def("views", &views);
   m.def("unobserved", &unobserved);
+  m.def("foreign", &foreign);
 }

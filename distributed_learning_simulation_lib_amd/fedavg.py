@@ -692,6 +692,16 @@ class FedAvgContext:
         _native.check(self._lib.fedavg_dyn_state(self._h, ctypes.byref(a), ctypes.byref(p)))
         return bool(a.value), int(p.value)
 
+    def dyn_configure(self, idle_us: int = 0, life_us: int = 0) -> None:
+        """The wave's idle limit / lifetime (µs) for the following launches (0: unchanged)."""
+        _native.check(self._lib.fedavg_dyn_configure(self._h, int(idle_us), int(life_us)))
+
+    def dyn_info(self) -> dict[str, int]:
+        """fedavg_dyn_info: the open wave's state and this context's continued waves / launches."""
+        v = (ctypes.c_int32 * 5)()
+        _native.check(self._lib.fedavg_dyn_info(self._h, v, 5))
+        return dict(zip(("active", "published", "base", "reopens", "launches"), (int(x) for x in v)))
+
     # -- fault reporting ---------------------------------------------------------------
     def flags(self) -> int:
         """Synchronise the stream and return the latched NaN flag bits."""

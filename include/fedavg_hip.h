@@ -474,7 +474,17 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
  *       it does not — the outputs are complete once the next fedavg_check on this context
  *       returns (it waits for the wave), which spares `stream` the cross-stream wait (a stream
  *       that waited on another's event can still read as busy right after its synchronize).
+ *       folded counts the caller's rows from 0 (every wave of the round, see below).
+ *   A wave that ended itself stays open for the caller: the next publication that hands over
+ *       rows launches a fresh wave continuing from the fp64 accumulator (its rows [0, folded) are
+ *       there) — the reference server's poll loop hands updates over in bursts with a sleep in
+ *       between (simulation_lib/server/server.py:133-146), and each burst after the idle limit is
+ *       folded while it arrives. Rows published to the ended wave after it stopped reading are
+ *       handed to the new one. The close divides by the totals of every published row.
  *   fedavg_dyn_state(ctx, &active, &published)
+ *   fedavg_dyn_info(ctx, info, n): the first n of {active, published, rows in the accumulator from
+ *       waves that ended themselves this round, continued waves (cumulative), wave launches
+ *       (cumulative)}.
  * Per element the fold is the reference's arrival-order chain (separately rounded product and
  * sum): the bits equal fedavg_aggregate's.
  * ===================================================================================== */
@@ -484,6 +494,10 @@ int32_t fedavg_dyn_publish(fedavg_ctx* ctx, const void* const* client_ptrs, cons
 int32_t fedavg_dyn_close(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dtype, int32_t join, void* stream,
                          int32_t* folded_out, int32_t* finalized_out);
 int32_t fedavg_dyn_state(const fedavg_ctx* ctx, int32_t* active, int32_t* published);
+int32_t fedavg_dyn_info(const fedavg_ctx* ctx, int32_t* info, int32_t n);
+/* The wave's idle limit and lifetime in microseconds for the following launches (0 keeps the
+ * current value; the defaults come from FEDAVG_DYN_IDLE_US / FEDAVG_DYN_LIFE_US, 500 us / 2 s). */
+int32_t fedavg_dyn_configure(fedavg_ctx* ctx, int64_t idle_us, int64_t life_us);
 /* With fedavg_prof_enable on: the summed time of the closed waves' body launches (enqueue at
  * the open to the launch's end, so the arrival phase is included) and their count; clears them. */
 int32_t fedavg_dyn_prof_collect(fedavg_ctx* ctx, double* total_ms, int32_t* waves);

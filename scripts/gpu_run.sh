@@ -8,6 +8,10 @@
 #   alias<G>              the single-process peer round rehearsed with G aliased entries on cuda:0
 #   plugin / gradient     bench.py --workload plugin / gradient
 #   plugin_static / gradient_static   the same with the dynamic wave off (FEDAVG_DYN=0)
+#   bursts / bursts_static / bursts_spin   plugin rounds in 4 bursts 2 ms apart (the reference server's
+#                         poll-then-sleep cadence): default wave / wave off / wave that never idles out
+#   idle=<us>             plugin + gradient lines with FEDAVG_DYN_IDLE_US=<us>
+#   cpu                   the headline line with its CPU baseline (pinned child process)
 #   pers_int / pers_float bench.py --workload personalized (integer / float weights)
 #   profile               scripts/profile.sh <out-tag> (kernel trace + FETCH/WRITE PMC passes)
 #   pers_pmc              scripts/gpu_pers_pmc.sh
@@ -45,6 +49,13 @@ for step in "$@"; do
     plugin) run plugin 300 python -u bench.py --workload plugin --no-cpu-baseline ;;
     gradient) run gradient 300 python -u bench.py --workload gradient --no-cpu-baseline ;;
     plugin_static) FEDAVG_DYN=0 run plugin_static 300 python -u bench.py --workload plugin --no-cpu-baseline ;;
+    bursts) run bursts 300 python -u bench.py --workload plugin --no-cpu-baseline --arrival bursts:4:2 ;;
+    bursts_static) FEDAVG_DYN=0 run bursts_static 300 python -u bench.py --workload plugin --no-cpu-baseline --arrival bursts:4:2 ;;
+    bursts_spin) FEDAVG_DYN_IDLE_US=1000000 run bursts_spin 300 python -u bench.py --workload plugin --no-cpu-baseline --arrival bursts:4:2 ;;
+    idle=*) I=${step#idle=}
+            FEDAVG_DYN_IDLE_US=$I run plugin_idle$I 300 python -u bench.py --workload plugin --no-cpu-baseline
+            FEDAVG_DYN_IDLE_US=$I run gradient_idle$I 300 python -u bench.py --workload gradient --no-cpu-baseline ;;
+    cpu) run cpu 400 python -u bench.py --no-probe --steps 5 --warmup 2 ;;
     gradient_static) FEDAVG_DYN=0 run gradient_static 300 python -u bench.py --workload gradient --no-cpu-baseline ;;
     pers_int) run pers_int 300 python -u bench.py --workload personalized --pers-weights int --no-cpu-baseline --no-probe ;;
     pers_float) run pers_float 300 python -u bench.py --workload personalized --pers-weights float --no-cpu-baseline --no-probe ;;

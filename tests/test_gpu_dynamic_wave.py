@@ -79,7 +79,7 @@ def test_small_rounds_skip_the_wave(hip_device, monkeypatch):
     for r, n in enumerate((8, 8, 20, 20)):
         _round(algo, hip_device, n, 40 + r)
     # round 0 (no history) and round 3 (after a 20-update round) open a wave; rounds 1-2 do not
-    assert algo.dyn_stats == {"waves": 2, "rows": 28, "finalized": 2}, algo.dyn_stats
+    assert _core(algo.dyn_stats) == {"waves": 2, "rows": 28, "finalized": 2}, algo.dyn_stats
     algo.exit()
 
 
@@ -87,7 +87,7 @@ def test_small_rounds_skip_the_wave(hip_device, monkeypatch):
 def test_fractional_weights_and_result_dtypes(hip_device, result_dtype):
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True, result_dtype=result_dtype)
     _round(algo, hip_device, 11, 5, weights="float")
-    assert algo.dyn_stats == {"waves": 1, "rows": 11, "finalized": 1}
+    assert _core(algo.dyn_stats) == {"waves": 1, "rows": 11, "finalized": 1}
     algo.exit()
 
 
@@ -100,7 +100,7 @@ def test_a_row_it_cannot_take_closes_it_early(hip_device):
 
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
     _round(algo, hip_device, 9, 21, mutate=mutate)
-    assert algo.dyn_stats == {"waves": 1, "rows": 4, "finalized": 0}
+    assert _core(algo.dyn_stats) == {"waves": 1, "rows": 4, "finalized": 0}
     algo.exit()
 
 
@@ -117,9 +117,14 @@ def test_busy_stream_defers_publication(hip_device):
     algo.exit()
 
 
+def _core(st):
+    return {k: st[k] for k in ("waves", "rows", "finalized")}
+
+
 def test_wave_ends_itself_when_arrivals_stop(hip_device, monkeypatch):
     # FEDAVG_DYN_IDLE_US=20000: a 200 ms gap between arrivals ends the wave with the rows it has;
-    # the later rows go through the ordinary waves
+    # the next publication continues the round in a fresh wave that starts from the accumulator,
+    # and that wave divides into the result
     monkeypatch.setenv("FEDAVG_DYN_IDLE_US", "20000")
     monkeypatch.setenv("FEDAVG_DYN_BATCH", "1")
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
@@ -131,9 +136,94 @@ def test_wave_ends_itself_when_arrivals_stop(hip_device, monkeypatch):
         return p
 
     _round(algo, hip_device, 8, 23, mutate=mutate)
-    # (a publication the current stream defers joins the next arrival's: 1-3 rows before the gap)
     st = algo.dyn_stats
-    assert st["waves"] == 1 and 1 <= st["rows"] <= 3 and st["finalized"] == 0, st
+    assert _core(st) == {"waves": 1, "rows": 8, "finalized": 1} and st["reopens"] == 1, st
+    algo.exit()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.float64])
+def test_bursts_close_reopen_close_at_the_default_idle_limit(hip_device, monkeypatch, dtype):
+    # the reference server's cadence (server.py:133-146: the arrivals of one poll back to back,
+    # then a sleep): 3 bursts of 5 with 5 ms gaps, far above the default 500 us idle limit. Each
+    # gap ends the wave; the burst after it is folded by a continued wave (from the accumulator);
+    # the last one divides. Bit-identical to the single chain.
+    monkeypatch.delenv("FEDAVG_DYN_IDLE_US")
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    assert algo.settings.dynamic.idle_us == 500
+
+    def mutate(k, p):
+        if k in (5, 10):
+            torch.cuda.synchronize()
+            time.sleep(0.005)
+        return p
+
+    for r in range(2):
+        _round(algo, hip_device, 15, 80 + r, dtype, mutate=mutate)
+    st = algo.dyn_stats
+    assert _core(st) == {"waves": 2, "rows": 30, "finalized": 2}, st
+    assert st["reopens"] >= 2, st  # at least one continued wave per round
+    algo.exit()
+
+
+def test_idle_before_the_aggregate_finalizes_from_the_accumulator(hip_device, monkeypatch):
+    # every row folded, then the wave idles out before aggregate_worker_data: the close finds it
+    # ended (rows in the accumulator) and the ordinary finalize divides — still bit-identical
+    monkeypatch.delenv("FEDAVG_DYN_IDLE_US")
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    orig = algo.aggregate_worker_data
+
+    def late():
+        torch.cuda.synchronize()
+        time.sleep(0.01)
+        return orig()
+
+    algo.aggregate_worker_data = late
+    # 5 rows: published at once, then in pairs — every row is out before the sleep (an unpublished
+    # last row would instead be handed to a continued wave, which then divides: the other test)
+    _round(algo, hip_device, 5, 90)
+    st = algo.dyn_stats
+    assert _core(st) == {"waves": 1, "rows": 5, "finalized": 0} and st["reopens"] == 0, st
+    algo.exit()
+
+
+def test_multi_wave_round_with_bursts(hip_device, monkeypatch):
+    # wave_size 6 and 17 updates in bursts: the dynamic wave (continued after a gap) takes the
+    # first 6, its flush leaves them in the accumulator, ordinary waves fold the rest
+    monkeypatch.delenv("FEDAVG_DYN_IDLE_US")
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True, wave_size=6)
+
+    def mutate(k, p):
+        if k in (3, 9):
+            torch.cuda.synchronize()
+            time.sleep(0.004)
+        return p
+
+    _round(algo, hip_device, 17, 91, mutate=mutate)
+    st = algo.dyn_stats
+    assert _core(st) == {"waves": 1, "rows": 6, "finalized": 0}, st
+    algo.exit()
+
+
+def test_many_small_tensors(hip_device):
+    # 1,500 tensors whose sizes are no multiple of the body tile: the edge launch has thousands of
+    # workgroups and may hold the GPU first; the mirror is elected from either launch
+    rng = np.random.default_rng(5)
+    shapes = {f"t{i}": (int(rng.integers(1, 9000)),) for i in range(1500)}
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    g = torch.Generator().manual_seed(12)
+    oracle = OracleFedAvg()
+    for k in range(5):
+        p = {name: torch.randn(s, generator=g) for name, s in shapes.items()}
+        w = 10 + 3 * k
+        algo.process_worker_data(k, ParameterMessage(parameter={m: t.to(hip_device) for m, t in p.items()},
+                                                     aggregation_weight=w))
+        oracle.process_worker_data(k, OracleMessage(parameter={m: t.numpy() for m, t in p.items()},
+                                                    aggregation_weight=w))
+    got = algo.aggregate_worker_data().parameter
+    want = oracle.aggregate_worker_data().parameter
+    for name, v in want.items():
+        assert bits_equal(got[name].cpu().numpy(), v), name
+    assert algo.dyn_stats["waves"] == 1 and algo.dyn_stats["rows"] == 5, algo.dyn_stats
     algo.exit()
 
 
@@ -223,8 +313,38 @@ def test_c_abi_protocol(hip_device):
         ctx.raise_on_nan()
         assert bits_equal(out.cpu().numpy(), want)
         ctx.reset()
+        # a wave that ends itself (1 ms idle limit) is continued by the next publication: rows
+        # [0, 3) from the accumulator, rows [3, 7) folded by the fresh launch, which divides
+        ctx.dyn_configure(idle_us=1000)
+        r0 = ctx.dyn_info()["reopens"]
+        ctx.dyn_open(torch.float32, 16)
+        torch.cuda.current_stream(hip_device).synchronize()
+        head3 = NativeClientTable(1, hip_device.index or 0)
+        for x, w in zip(dev[:3], ws[:3]):
+            head3.add_client([x], [w])
+        assert ctx.dyn_publish(head3) == 3
+        time.sleep(0.02)  # the wave ends itself
+        assert ctx.dyn_publish(table) == 4
+        info = ctx.dyn_info()
+        assert info["reopens"] == r0 + 1 and info["base"] == 3 and info["active"] == 1, info
+        out.fill_(float("nan"))
+        assert ctx.dyn_close(outs, torch.float64) == (7, True)
+        ctx.raise_on_nan()
+        assert bits_equal(out.cpu().numpy(), want)
+        # ... and one that ends itself with nothing published is continued zero-initialised
+        ctx.dyn_open(torch.float32, 16)
+        time.sleep(0.02)
+        torch.cuda.current_stream(hip_device).synchronize()
+        assert ctx.dyn_publish(table) == 7
+        assert ctx.dyn_info()["base"] == 0
+        out.fill_(float("nan"))
+        assert ctx.dyn_close(outs, torch.float64) == (7, True)
+        ctx.raise_on_nan()
+        assert bits_equal(out.cpu().numpy(), want)
+        ctx.reset()
     finally:
         ctx.close()
+
 
 
 def test_fresh_contexts_back_to_back(hip_device):

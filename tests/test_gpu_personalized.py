@@ -252,10 +252,16 @@ def test_result_buffers_reused_only_when_unobserved(hip_device):
     import torch.multiprocessing as _torch_mp  # noqa: F401  (registers the tensor reducers)
 
     sent = res3.worker_data[3].parameter["fc"].data_ptr()
+    sent_sum = sum(float(t.double().sum().item()) for t in res3.worker_data[3].parameter.values())
     payload = ForkingPickler.dumps(res3.worker_data[3].parameter)
     del res3
     gc.collect()
     res4, _ = one_round(4)
     assert res4.worker_data[3].parameter["fc"].data_ptr() != sent
+    # the consumer rebuilds and releases it, so the IPC limbo drains before this process ends
+    from tests.ipc_consumer import hand_over
+
+    assert abs(hand_over(bytes(payload)) - sent_sum) <= 1e-9 * (1 + abs(sent_sum))
     del payload
+    torch.cuda.ipc_collect()
     algo.exit()

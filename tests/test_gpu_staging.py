@@ -242,10 +242,16 @@ def test_result_buffer_reuse_never_changes_a_kept_result(hip_device, devices):
     import torch.multiprocessing as _torch_mp  # noqa: F401  (registers the tensor reducers)
 
     sent_ptr = again["fc"].data_ptr()
+    sent_sum = float(again["fc"].double().sum().item())
     payload = ForkingPickler.dumps(again["fc"])
     del again
     gc.collect()
     fresh, _ = one_round(30)
     assert fresh["fc"].data_ptr() != sent_ptr
+    # the consumer rebuilds and releases it (reads the round-20 result), so the IPC limbo drains
+    from tests.ipc_consumer import hand_over
+
+    assert abs(hand_over(bytes(payload)) - sent_sum) <= 1e-9 * (1 + abs(sent_sum))
     del payload
+    torch.cuda.ipc_collect()
     algo.exit()

@@ -1132,6 +1132,25 @@ def main_plugin(args: argparse.Namespace) -> int:
     kernel_ms, launches = ctx.prof_collect()
     dyn_ms, dyn_waves = ctx.dyn_prof_collect()
     dyn = {k: round((algo.dyn_stats[k] - dyn0[k]) / args.steps, 2) for k in dyn0}
+    host_timed, tail_timed = host_s[0], tail_s[0]
+    if dyn_waves and not args.no_kernel_events:
+        # after the timed region: the same rounds again, each wave's tiles recording when they
+        # finished (fedavg_dyn_timing, GPU clock): the fold after the last rows reached the tiles
+        # (result stores included) and after the close, medians over the rounds
+        dyn_t: dict[str, list[float]] = {"rows_to_end_us": [], "close_to_end_us": []}
+        ctx.prof_enable(True)
+        for _ in range(min(args.steps, 10)):
+            step()
+            tm = algo._context().dyn_timing()
+            for key in dyn_t:
+                if tm[key] >= 0:
+                    dyn_t[key].append(tm[key])
+        ctx.prof_enable(False)
+        ctx.prof_collect()
+        ctx.dyn_prof_collect()
+        host_s[0], tail_s[0] = host_timed, tail_timed  # the timed rounds' host times only
+        for key, vals in dyn_t.items():
+            dyn[key.replace("_us", "_ms_median")] = round(float(np.median(vals)) / 1e3, 4) if vals else None
     in_b, out_b = in_dtype.itemsize, out_dtype.itemsize
     job_bytes = N * P * in_b + P * out_b
     n_waves = -(-N // wave)
@@ -1148,6 +1167,9 @@ def main_plugin(args: argparse.Namespace) -> int:
         kstep_s = dyn_ms * 1e-3 / args.steps
         launch_bytes = job_bytes
         achieved = launch_bytes / kstep_s / 1e9 if kstep_s > 0 else 0.0
+    # the HBM probes (read / copy ceilings; their known byte counts calibrate a PMC pass's
+    # FETCH_SIZE / WRITE_SIZE in the same process, scripts/dyn_traffic.sh)
+    probe = None if args.no_probe else hbm_probes(device)
     burst = None
     if bursts > 1:
         # one burst's clients folded by the one-launch kernel (HIP events): the fold time the
@@ -1230,6 +1252,7 @@ def main_plugin(args: argparse.Namespace) -> int:
                        if dyn_rows_all else f"fedavg_tile_kernel x {n_waves} launch(es) per round"),
             "bytes_per_step": launch_bytes,
             "kernel_ms_per_step": round(kstep_s * 1e3, 4), "launches": launches + dyn_waves},
+        "hbm_probe": probe,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

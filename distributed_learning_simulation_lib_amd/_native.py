@@ -154,6 +154,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "fedavg_dyn_state": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "fedavg_dyn_info": (c_int32, [c_void_p, POINTER(c_int32), c_int32]),
     "fedavg_dyn_configure": (c_int32, [c_void_p, c_int64, c_int64]),
+    "fedavg_dyn_timing": (c_int32, [c_void_p, POINTER(c_double), c_int32]),
     "fedavg_dyn_prof_collect": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int32)]),
     # single-process multi-device mode (multi_device.cpp)
     "fedavg_multi_create": (c_int32, [POINTER(c_void_p), POINTER(c_int32), c_int32, POINTER(c_int64), c_int32, _PP]),

@@ -888,6 +888,7 @@ struct DynAck {     // host-coherent, written by the mirror workgroup
   uint32_t polls;   // the mirror's polls of the host word (FEDAVG_DYN_TRACE)
   uint64_t t_seen;  // s_memrealtime when the mirror saw the close, and when it acknowledged it
   uint64_t t_done;
+  uint64_t t_rows;  // s_memrealtime when the mirror last handed the tiles more rows
 };
 struct DynMirror {  // device memory, written by the mirror workgroup: one copy per XCD (kDynCopies,
   uint64_t word;    // a cache line apart), so the tile workgroups' polls spread over 8 lines
@@ -918,6 +919,8 @@ struct DynArgs {
   uint64_t* outs;
   DynMirror* mir;
   uint32_t* elect;          // the mirror election word (device memory): the wave's epoch once taken
+  uint64_t* tend;           // profiling: per tile (body tiles, then edge tiles) the time it finished
+  int32_t edge_base;        // the first edge tile's index in tend
   int32_t num_tiles;
   int32_t num_segs;
   int32_t cap;
@@ -966,7 +969,7 @@ __device__ void dyn_mirror(const DynArgs& a) {
   __shared__ uint32_t s_cmd[3];  // rows published, 0 running / 1 host close / 2 own close, close mode
   const int tid = static_cast<int>(threadIdx.x);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t last = t0, t_seen = 0;
+  uint64_t last = t0, t_seen = 0, t_rows = 0;
   uint32_t mc = 0, polls = 0;  // rows mirrored so far, host polls
   for (;;) {
     if (tid == 0) {
@@ -1007,6 +1010,7 @@ __device__ void dyn_mirror(const DynArgs& a) {
     const uint32_t hc = s_cmd[0], st = s_cmd[1], mode = s_cmd[2];
     // copy rows [mc, hc) of the host table, and at a final close the divisors and outputs
     const int rows = static_cast<int>(hc - mc);
+    if (rows > 0) t_rows = __builtin_amdgcn_s_memrealtime();
     if (rows > 0) {
       const int n = rows * a.num_segs;
 #pragma unroll 4
@@ -1035,6 +1039,7 @@ __device__ void dyn_mirror(const DynArgs& a) {
       if (st != 0) {
         __hip_atomic_store(&a.ack->polls, polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.ack->t_seen, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ack->t_rows, t_rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.ack->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.ack->word, static_cast<uint64_t>(st) | (static_cast<uint64_t>(hc) << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1132,6 +1137,39 @@ __device__ __forceinline__ void dyn_prime(DynV<T> (&buf)[NB], gptr<const DynV<T>
   for (int v = 0; v + 1 < NB; ++v) dyn_issue<T, PART>(buf[v], base, v, li, nfull);
 }
 
+// Look-ahead (FEDAVG_DYN_LOOKAHEAD, A/B knob): before a batch's last row is folded, one relaxed
+// poll of the mirror word; when the mirror has published the next row already, its table entry is
+// read and the last row's fold prefetches the next row's first vectors, so the load ring does not
+// drain between batches (the next batch skips its prime).
+#ifndef FEDAVG_DYN_LOOKAHEAD
+#define FEDAVG_DYN_LOOKAHEAD 0
+#endif
+constexpr bool kDynLookahead = FEDAVG_DYN_LOOKAHEAD != 0;
+
+__device__ __forceinline__ uint64_t dyn_rfl64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+// the client pointer of `row` for segment `seg` when the mirror has published it (0 otherwise),
+// and the mirror's row count through `count` (wave-uniform)
+__device__ __forceinline__ uint64_t dyn_peek(const DynArgs& a, const DynMirror* mir, int seg, int row, uint32_t& count) {
+  const uint64_t w = dyn_rfl64(__hip_atomic_load(&mir->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (static_cast<uint32_t>(w >> 32) != a.epoch) return 0;
+  const uint32_t c = static_cast<uint32_t>(w) & 0xffffffu;
+  if (c <= static_cast<uint32_t>(row)) return 0;
+  count = c;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return dyn_rfl64(dyn_ld_sys64(a.ptab + static_cast<int64_t>(seg) * a.cap + row));
+}
+
+// While the context profiles (fedavg_prof_enable): every tile workgroup stores the time it finished
+// (its result stores issued) into tend[tile] — plain stores, no atomics — and fedavg_dyn_timing
+// takes the latest: the fold time after the last rows reached the tiles. One lane.
+__device__ __forceinline__ void dyn_tile_done(const DynArgs& a, int tile) {
+  if (a.tend) a.tend[tile] = __builtin_amdgcn_s_memrealtime();
+}
+
 // EDGE = false: the body tiles, workgroup 0 the mirror; EDGE = true: the edge tiles
 template <typename T, bool EDGE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kDynLanes, kDynLanes), amdgpu_waves_per_eu(2, 8)))
@@ -1198,6 +1236,9 @@ void dyn_wave_kernel(DynArgs a) {
   uint32_t closed = 0;   // the mirror closed the wave (thread 0)
   uint32_t cmode = OUT_ACC;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NB = G::NB;
+  V buf[NB];
+  bool primed = false;  // the ring already holds row k's first vectors (look-ahead)
   for (;;) {
     if (threadIdx.x == 0) {
       if (avail <= static_cast<uint32_t>(k) && !closed) {
@@ -1249,14 +1290,34 @@ void dyn_wave_kernel(DynArgs a) {
       return to_global<T>(reinterpret_cast<const void*>(((static_cast<uint64_t>(hi) << 32) | lo) + elem_off));
     };
     if (EDGE ? nfull > 0 : true) {  // the tile's whole vectors (all of a body tile's)
-      constexpr int NB = G::NB;
-      V buf[NB];
-      dyn_prime<T, EDGE, NB>(buf, (gptr<const V>)client(0), li, nfull);
-      int i = 0;
-      for (; i + 1 < n; ++i)
-        dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i + 1), sw[i], li,
-                                               nfull);
-      dyn_fold_client<T, AE, EDGE, false, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i), sw[i], li, nfull);
+      if (!primed) dyn_prime<T, EDGE, NB>(buf, (gptr<const V>)client(0), li, nfull);
+      if constexpr (kDynLookahead) {
+        // one call site: every row prefetches a successor — the batch's next row, at the batch's end
+        // the mirror's next row when published (peeked), else its own first vectors again (L2 hits;
+        // the next batch primes afresh)
+        bool ahead = false;
+        for (int i = 0; i < n; ++i) {
+          gptr<const T> nx;
+          if (i + 1 < n) {
+            nx = client(i + 1);
+          } else {
+            uint32_t c = 0;
+            const uint64_t p = __builtin_amdgcn_readfirstlane(closed) ? 0 : dyn_peek(a, mir, seg, k + n, c);
+            ahead = p != 0;
+            if (ahead && threadIdx.x == 0 && c > avail) avail = c;
+            nx = ahead ? to_global<T>(reinterpret_cast<const void*>(p + elem_off)) : client(i);
+          }
+          dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)nx, sw[i], li, nfull);
+        }
+        primed = ahead;
+      } else {
+        int i = 0;
+        for (; i + 1 < n; ++i)
+          dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i + 1), sw[i],
+                                                 li, nfull);
+        dyn_fold_client<T, AE, EDGE, false, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i), sw[i], li,
+                                                nfull);
+      }
     }
     if constexpr (EDGE) {
       if (tail > 0 && li == 0) {  // the < N elements past them, one lane, accumulators in LDS
@@ -1284,7 +1345,10 @@ void dyn_wave_kernel(DynArgs a) {
   // (a partial tile: its whole vectors here, its tail elements from LDS below)
   bool bad_acc = false, bad_res = false;
   const bool final_close = mode != OUT_ACC;
-  if (!final_close && k == 0) return;  // nothing folded: the accumulator holds nothing for this round
+  if (!final_close && k == 0) {  // nothing folded: the accumulator holds nothing new for this round
+    if (li == 0) dyn_tile_done(a, EDGE ? a.edge_base + static_cast<int>(blockIdx.x) - 1 : static_cast<int>(blockIdx.x) - 1);
+    return;
+  }
   const double W = final_close ? s_W : 1.0;
   void* const out_raw = final_close ? reinterpret_cast<void*>(s_out) : reinterpret_cast<void*>(a.acc + acc_base);
   const int64_t out_off = final_close ? td.start : 0;
@@ -1346,6 +1410,7 @@ void dyn_wave_kernel(DynArgs a) {
     if (ba) raise_flag(a.flag, 0);
     if (br) raise_flag(a.flag, 1);
   }
+  if (li == 0) dyn_tile_done(a, EDGE ? a.edge_base + static_cast<int>(blockIdx.x) - 1 : static_cast<int>(blockIdx.x) - 1);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2251,6 +2316,8 @@ struct fedavg_ctx {
     std::vector<double> wsum_base;
     int32_t reopens = 0;   // continued waves, cumulative (fedavg_dyn_info)
     int32_t launches = 0;  // wave launches, cumulative
+    uint64_t* tend = nullptr;  // profiling: each tile's finishing time (dyn_tile_done)
+    bool timed = false;        // the last launch recorded them
     uint64_t idle_ticks = 0, life_ticks = 0;
   } dyn;
 };
@@ -3179,6 +3246,7 @@ int32_t fedavg_ctx_destroy(fedavg_ctx* c) {
   (void)hipDeviceSynchronize();
   if (c->dyn.host) (void)hipHostFree(c->dyn.host);
   if (c->dyn.mirror) (void)hipFree(c->dyn.mirror);
+  if (c->dyn.tend) (void)hipFree(c->dyn.tend);
   if (c->dyn.dtab) (void)hipFree(c->dyn.dtab);
   if (c->dyn.d_tiles) (void)hipFree(c->dyn.d_tiles);
   if (c->dyn.d_edge_tiles) (void)hipFree(c->dyn.d_edge_tiles);
@@ -4200,6 +4268,13 @@ int32_t dyn_launch(fedavg_ctx* c, int32_t resume) {
   a.ptab = reinterpret_cast<uint64_t*>(d.dtab + L.ptab);
   a.mir = reinterpret_cast<DynMirror*>(d.mirror);
   a.elect = reinterpret_cast<uint32_t*>(d.mirror + sizeof(DynMirror) * kDynCopies);
+  a.edge_base = static_cast<int32_t>(d.tiles.size());
+  a.tend = nullptr;
+  if (c->prof) {
+    if (!d.tend) FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.tend), sizeof(uint64_t) * (d.tiles.size() + d.edge_tiles.size())));
+    a.tend = d.tend;
+  }
+  d.timed = c->prof;
   a.num_tiles = static_cast<int32_t>(d.tiles.size());
   a.num_segs = c->T;
   a.cap = d.cap;
@@ -4284,6 +4359,7 @@ int32_t dyn_continue(fedavg_ctx* c) {
   }
   d.base += folded;
   __atomic_store_n(&ack->word, uint64_t{0}, __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->t_rows, uint64_t{0}, __ATOMIC_RELAXED);
   __atomic_store_n(&ack->error, 0u, __ATOMIC_RELAXED);
   __atomic_store_n(&ctl->word, dyn_word(static_cast<uint32_t>(left), 0u, OUT_ACC, 0u), __ATOMIC_RELEASE);
   ++d.reopens;
@@ -4362,6 +4438,7 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
   DynAck* ack = reinterpret_cast<DynAck*>(d.host + L.ack);
   __atomic_store_n(&ctl->word, dyn_word(0u, 0u, OUT_ACC, 0u), __ATOMIC_RELAXED);
   __atomic_store_n(&ack->word, uint64_t{0}, __ATOMIC_RELAXED);
+  __atomic_store_n(&ack->t_rows, uint64_t{0}, __ATOMIC_RELAXED);
   __atomic_store_n(&ack->error, 0u, __ATOMIC_RELEASE);
   d.wsum.assign(c->T, -0.0);
   d.wsum_base.assign(c->T, -0.0);
@@ -4525,6 +4602,29 @@ int32_t fedavg_dyn_configure(fedavg_ctx* c, int64_t idle_us, int64_t life_us) {
   if (idle_us < 0 || life_us < 0) return fail(FEDAVG_ERR_INVALID, "idle / life limits must be >= 0");
   if (idle_us) c->dyn.idle_ticks = static_cast<uint64_t>(idle_us) * 100;  // s_memrealtime: 100 MHz
   if (life_us) c->dyn.life_ticks = static_cast<uint64_t>(life_us) * 100;
+  return FEDAVG_OK;
+}
+
+int32_t fedavg_dyn_timing(const fedavg_ctx* c, double* out, int32_t n) {
+  FEDAVG_RET(check_ctx(c));
+  const auto& d = c->dyn;
+  double v[3] = {-1.0, -1.0, -1.0};
+  if (d.host && d.timed && d.tend && !d.active) {
+    FEDAVG_HIP_TRY(hipSetDevice(c->device));
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.stream));
+    FEDAVG_HIP_TRY(hipStreamSynchronize(d.edge_stream));
+    std::vector<uint64_t> te(d.tiles.size() + d.edge_tiles.size());
+    FEDAVG_HIP_TRY(hipMemcpy(te.data(), d.tend, sizeof(uint64_t) * te.size(), hipMemcpyDeviceToHost));
+    const uint64_t t_end = te.empty() ? 0 : *std::max_element(te.begin(), te.end());
+    const DynLayout L(c->T, d.cap);
+    const DynAck* ack = reinterpret_cast<const DynAck*>(d.host + L.ack);
+    const uint64_t t_rows = __atomic_load_n(&ack->t_rows, __ATOMIC_RELAXED);
+    const uint64_t t_seen = __atomic_load_n(&ack->t_seen, __ATOMIC_RELAXED);
+    if (t_end && t_rows && t_end >= t_rows) v[0] = static_cast<double>(t_end - t_rows) / 100.0;  // 100 MHz
+    if (t_end && t_seen && t_end >= t_seen) v[1] = static_cast<double>(t_end - t_seen) / 100.0;
+    if (t_seen && t_rows) v[2] = (static_cast<double>(t_seen) - static_cast<double>(t_rows)) / 100.0;
+  }
+  for (int32_t i = 0; i < n && i < 3; ++i) out[i] = v[i];
   return FEDAVG_OK;
 }
 

@@ -696,6 +696,12 @@ class FedAvgContext:
         """The wave's idle limit / lifetime (µs) for the following launches (0: unchanged)."""
         _native.check(self._lib.fedavg_dyn_configure(self._h, int(idle_us), int(life_us)))
 
+    def dyn_timing(self) -> dict[str, float]:
+        """fedavg_dyn_timing of the last completed wave (µs, GPU clock; -1 where not recorded)."""
+        v = (ctypes.c_double * 3)()
+        _native.check(self._lib.fedavg_dyn_timing(self._h, v, 3))
+        return dict(zip(("rows_to_end_us", "close_to_end_us", "rows_to_close_us"), (float(x) for x in v)))
+
     def dyn_info(self) -> dict[str, int]:
         """fedavg_dyn_info: the open wave's state and this context's continued waves / launches."""
         v = (ctypes.c_int32 * 5)()

@@ -495,6 +495,12 @@ int32_t fedavg_dyn_close(fedavg_ctx* ctx, void* const* out_ptrs, int32_t out_dty
                          int32_t* folded_out, int32_t* finalized_out);
 int32_t fedavg_dyn_state(const fedavg_ctx* ctx, int32_t* active, int32_t* published);
 int32_t fedavg_dyn_info(const fedavg_ctx* ctx, int32_t* info, int32_t n);
+/* GPU-clock timing of the context's last wave when it ran with fedavg_prof_enable on (each tile
+ * workgroup then stores its finishing time; this call waits for the wave and reads them): the first
+ * n of {µs from the mirror handing the tiles their last rows to the wave's last workgroup finishing
+ * (the fold after the last publication, result stores included), µs from the mirror seeing the
+ * close to that end, µs from the last rows to the close} — -1 where not recorded. */
+int32_t fedavg_dyn_timing(const fedavg_ctx* ctx, double* out, int32_t n);
 /* The wave's idle limit and lifetime in microseconds for the following launches (0 keeps the
  * current value; the defaults come from FEDAVG_DYN_IDLE_US / FEDAVG_DYN_LIFE_US, 500 us / 2 s). */
 int32_t fedavg_dyn_configure(fedavg_ctx* ctx, int64_t idle_us, int64_t life_us);

@@ -118,7 +118,12 @@ def main() -> int:
     ap.add_argument("--match", default="")
     ap.add_argument("--json", default=None)
     ap.add_argument("--isa", default=None)
+    ap.add_argument("--lib", default=None, help="another build of the library (a tuning variant)")
     args = ap.parse_args()
+    if args.lib:
+        global LIB
+        LIB = Path(args.lib).resolve()
+        code_objects.__defaults__ = (LIB, "gfx950")
     if args.isa:
         print(disassemble(args.isa))
         return 0

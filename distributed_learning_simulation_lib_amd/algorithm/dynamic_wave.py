@@ -42,7 +42,7 @@ class DynamicWaveSettings:
       training kernels that must never wait should turn it off.
     * ``batch`` (``FEDAVG_DYN_BATCH``, 2): staged rows handed over per publication (the first at once).
     * ``min_rows`` (``FEDAVG_DYN_MIN_ROWS``, 4): a round after one of fewer updates skips the wave.
-    * ``idle_us`` (``FEDAVG_DYN_IDLE_US``, 500): the wave ends itself after this long without a row,
+    * ``idle_us`` (``FEDAVG_DYN_IDLE_US``, 200): the wave ends itself after this long without a row,
       freeing the GPU between bursts; the next publication continues it from the accumulator.
     * ``life_us`` (``FEDAVG_DYN_LIFE_US``, 2 s): the longest one launch spins; likewise continued.
     """
@@ -50,7 +50,7 @@ class DynamicWaveSettings:
     enabled: bool = True
     batch: int = 2
     min_rows: int = 4
-    idle_us: int = 500
+    idle_us: int = 200
     life_us: int = 2_000_000
 
     def __post_init__(self) -> None:

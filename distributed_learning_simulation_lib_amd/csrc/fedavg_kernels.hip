@@ -1137,32 +1137,6 @@ __device__ __forceinline__ void dyn_prime(DynV<T> (&buf)[NB], gptr<const DynV<T>
   for (int v = 0; v + 1 < NB; ++v) dyn_issue<T, PART>(buf[v], base, v, li, nfull);
 }
 
-// Look-ahead (FEDAVG_DYN_LOOKAHEAD, A/B knob): before a batch's last row is folded, one relaxed
-// poll of the mirror word; when the mirror has published the next row already, its table entry is
-// read and the last row's fold prefetches the next row's first vectors, so the load ring does not
-// drain between batches (the next batch skips its prime).
-#ifndef FEDAVG_DYN_LOOKAHEAD
-#define FEDAVG_DYN_LOOKAHEAD 0
-#endif
-constexpr bool kDynLookahead = FEDAVG_DYN_LOOKAHEAD != 0;
-
-__device__ __forceinline__ uint64_t dyn_rfl64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
-  return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-// the client pointer of `row` for segment `seg` when the mirror has published it (0 otherwise),
-// and the mirror's row count through `count` (wave-uniform)
-__device__ __forceinline__ uint64_t dyn_peek(const DynArgs& a, const DynMirror* mir, int seg, int row, uint32_t& count) {
-  const uint64_t w = dyn_rfl64(__hip_atomic_load(&mir->word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (static_cast<uint32_t>(w >> 32) != a.epoch) return 0;
-  const uint32_t c = static_cast<uint32_t>(w) & 0xffffffu;
-  if (c <= static_cast<uint32_t>(row)) return 0;
-  count = c;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return dyn_rfl64(dyn_ld_sys64(a.ptab + static_cast<int64_t>(seg) * a.cap + row));
-}
-
 // While the context profiles (fedavg_prof_enable): every tile workgroup stores the time it finished
 // (its result stores issued) into tend[tile] — plain stores, no atomics — and fedavg_dyn_timing
 // takes the latest: the fold time after the last rows reached the tiles. One lane.
@@ -1236,9 +1210,6 @@ void dyn_wave_kernel(DynArgs a) {
   uint32_t closed = 0;   // the mirror closed the wave (thread 0)
   uint32_t cmode = OUT_ACC;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  constexpr int NB = G::NB;
-  V buf[NB];
-  bool primed = false;  // the ring already holds row k's first vectors (look-ahead)
   for (;;) {
     if (threadIdx.x == 0) {
       if (avail <= static_cast<uint32_t>(k) && !closed) {
@@ -1290,34 +1261,14 @@ void dyn_wave_kernel(DynArgs a) {
       return to_global<T>(reinterpret_cast<const void*>(((static_cast<uint64_t>(hi) << 32) | lo) + elem_off));
     };
     if (EDGE ? nfull > 0 : true) {  // the tile's whole vectors (all of a body tile's)
-      if (!primed) dyn_prime<T, EDGE, NB>(buf, (gptr<const V>)client(0), li, nfull);
-      if constexpr (kDynLookahead) {
-        // one call site: every row prefetches a successor — the batch's next row, at the batch's end
-        // the mirror's next row when published (peeked), else its own first vectors again (L2 hits;
-        // the next batch primes afresh)
-        bool ahead = false;
-        for (int i = 0; i < n; ++i) {
-          gptr<const T> nx;
-          if (i + 1 < n) {
-            nx = client(i + 1);
-          } else {
-            uint32_t c = 0;
-            const uint64_t p = __builtin_amdgcn_readfirstlane(closed) ? 0 : dyn_peek(a, mir, seg, k + n, c);
-            ahead = p != 0;
-            if (ahead && threadIdx.x == 0 && c > avail) avail = c;
-            nx = ahead ? to_global<T>(reinterpret_cast<const void*>(p + elem_off)) : client(i);
-          }
-          dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)nx, sw[i], li, nfull);
-        }
-        primed = ahead;
-      } else {
-        int i = 0;
-        for (; i + 1 < n; ++i)
-          dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i + 1), sw[i],
-                                                 li, nfull);
-        dyn_fold_client<T, AE, EDGE, false, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i), sw[i], li,
-                                                nfull);
-      }
+      constexpr int NB = G::NB;
+      V buf[NB];
+      dyn_prime<T, EDGE, NB>(buf, (gptr<const V>)client(0), li, nfull);
+      int i = 0;
+      for (; i + 1 < n; ++i)
+        dyn_fold_client<T, AE, EDGE, true, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i + 1), sw[i], li,
+                                               nfull);
+      dyn_fold_client<T, AE, EDGE, false, NB>(acc, buf, (gptr<const V>)client(i), (gptr<const V>)client(i), sw[i], li, nfull);
     }
     if constexpr (EDGE) {
       if (tail > 0 && li == 0) {  // the < N elements past them, one lane, accumulators in LDS
@@ -4408,7 +4359,7 @@ int32_t fedavg_dyn_open(fedavg_ctx* c, int32_t in_dtype, int32_t max_clients, vo
       FEDAVG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(dev), sizeof(TileDesc) * host->size()));
       FEDAVG_HIP_TRY(hipMemcpy(*dev, host->data(), sizeof(TileDesc) * host->size(), hipMemcpyHostToDevice));
     }
-    if (!d.idle_ticks) d.idle_ticks = dyn_env_us("FEDAVG_DYN_IDLE_US", 500) * 100;  // s_memrealtime: 100 MHz
+    if (!d.idle_ticks) d.idle_ticks = dyn_env_us("FEDAVG_DYN_IDLE_US", 200) * 100;  // s_memrealtime: 100 MHz
     if (!d.life_ticks) d.life_ticks = dyn_env_us("FEDAVG_DYN_LIFE_US", 2000000) * 100;
   }
   if (d.cap < max_clients) {

@@ -467,7 +467,7 @@ int32_t fedavg_sharded_round_edges(fedavg_comm* comm, fedavg_ctx* ctx, fedavg_pl
  *       fix the count. With out_ptrs (16-B aligned) the wave divides by the published rows'
  *       totals (arrival order) into the outputs: finalized = 1, the round is done (check with
  *       fedavg_check on `stream`). Otherwise — NULL outputs, or the wave ended itself after
- *       FEDAVG_DYN_IDLE_US (500) µs without a new row or FEDAVG_DYN_LIFE_US (2 s) in all — it
+ *       FEDAVG_DYN_IDLE_US (200) µs without a new row or FEDAVG_DYN_LIFE_US (2 s) in all — it
  *       stores the fp64 accumulator of rows [0, folded) (the context's state says so) and the
  *       caller folds rows [folded, K) with the ordinary calls; `stream` then continues after the
  *       wave. A finalized wave with join = 1 likewise orders `stream` after it; with join = 0
@@ -502,7 +502,7 @@ int32_t fedavg_dyn_info(const fedavg_ctx* ctx, int32_t* info, int32_t n);
  * close to that end, µs from the last rows to the close} — -1 where not recorded. */
 int32_t fedavg_dyn_timing(const fedavg_ctx* ctx, double* out, int32_t n);
 /* The wave's idle limit and lifetime in microseconds for the following launches (0 keeps the
- * current value; the defaults come from FEDAVG_DYN_IDLE_US / FEDAVG_DYN_LIFE_US, 500 us / 2 s). */
+ * current value; the defaults come from FEDAVG_DYN_IDLE_US / FEDAVG_DYN_LIFE_US, 200 us / 2 s). */
 int32_t fedavg_dyn_configure(fedavg_ctx* ctx, int64_t idle_us, int64_t life_us);
 /* With fedavg_prof_enable on: the summed time of the closed waves' body launches (enqueue at
  * the open to the launch's end, so the arrival phase is included) and their count; clears them. */

@@ -144,12 +144,12 @@ def test_wave_ends_itself_when_arrivals_stop(hip_device, monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.float64])
 def test_bursts_close_reopen_close_at_the_default_idle_limit(hip_device, monkeypatch, dtype):
     # the reference server's cadence (server.py:133-146: the arrivals of one poll back to back,
-    # then a sleep): 3 bursts of 5 with 5 ms gaps, far above the default 500 us idle limit. Each
+    # then a sleep): 3 bursts of 5 with 5 ms gaps, far above the default 200 us idle limit. Each
     # gap ends the wave; the burst after it is folded by a continued wave (from the accumulator);
     # the last one divides. Bit-identical to the single chain.
     monkeypatch.delenv("FEDAVG_DYN_IDLE_US")
     algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
-    assert algo.settings.dynamic.idle_us == 500
+    assert algo.settings.dynamic.idle_us == 200
 
     def mutate(k, p):
         if k in (5, 10):
@@ -328,6 +328,9 @@ def test_c_abi_protocol(hip_device):
         info = ctx.dyn_info()
         assert info["reopens"] == r0 + 1 and info["base"] == 3 and info["active"] == 1, info
         out.fill_(float("nan"))
+        # (the fill runs on the caller's stream, the wave on its own: the fill must be done before
+        # the close lets the wave store, or it may run after the wave and overwrite the result)
+        torch.cuda.current_stream(hip_device).synchronize()
         assert ctx.dyn_close(outs, torch.float64) == (7, True)
         ctx.raise_on_nan()
         assert bits_equal(out.cpu().numpy(), want)
@@ -338,6 +341,9 @@ def test_c_abi_protocol(hip_device):
         assert ctx.dyn_publish(table) == 7
         assert ctx.dyn_info()["base"] == 0
         out.fill_(float("nan"))
+        # (the fill runs on the caller's stream, the wave on its own: the fill must be done before
+        # the close lets the wave store, or it may run after the wave and overwrite the result)
+        torch.cuda.current_stream(hip_device).synchronize()
         assert ctx.dyn_close(outs, torch.float64) == (7, True)
         ctx.raise_on_nan()
         assert bits_equal(out.cpu().numpy(), want)

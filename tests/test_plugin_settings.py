@@ -12,7 +12,7 @@ def test_defaults_without_environment():
     s = PluginSettings.from_env({})
     assert s == PluginSettings()
     assert (s.wave_size, s.wave_min, s.eager_nan_check, s.qsgd_host_pointers) == (64, 0, False, True)
-    assert s.dynamic == DynamicWaveSettings(enabled=True, batch=2, min_rows=4, idle_us=500, life_us=2_000_000)
+    assert s.dynamic == DynamicWaveSettings(enabled=True, batch=2, min_rows=4, idle_us=200, life_us=2_000_000)
 
 
 def test_every_knob_from_the_environment():

@@ -40,30 +40,26 @@ read_corr = PROBE / (statistics.median(counter(f"{name}_fetch", "bw_read_kernel"
 write_corr = PROBE / (statistics.median(counter(f"{name}_write", "bw_copy_kernel")) * 1024)
 
 
-def per_kind(pass_dir: str) -> dict[str, list[float]]:
+def per_kind(pass_dir: str, fname: str = "run_counter_collection.csv", value=lambda r: float(r["Counter_Value"])):
+    """The dyn_wave_kernel dispatches split into body / edge launches (names are truncated by -T:
+    the body launch is the one with the larger grid — a workgroup per 6,144-element body tile)."""
+    dyn = [r for r in rows(pass_dir, fname) if "dyn_wave_kernel" in r["Kernel_Name"]]
+    body_grid = max((int(r.get("Grid_Size") or r["Grid_Size_X"]) for r in dyn), default=0)
     out: dict[str, list[float]] = {"body": [], "edge": []}
-    for r in rows(pass_dir):
-        k = r["Kernel_Name"]
-        if "dyn_wave_kernel" in k:
-            out["edge" if "true" in k.split("dyn_wave_kernel", 1)[1][:40] else "body"].append(float(r["Counter_Value"]))
+    for r in dyn:
+        out["body" if int(r.get("Grid_Size") or r["Grid_Size_X"]) == body_grid else "edge"].append(value(r))
     return out
 
 
 fetch, write = per_kind(f"{name}_fetch"), per_kind(f"{name}_write")
-rounds = len(fetch["body"])  # one body launch per round (continued waves would add launches: see waves_per_round)
+# one body launch per wave; a round's wave is continued (another launch pair) reopens times
+n_rounds = len(fetch["body"]) / (1.0 + (line["config"].get("dynamic_wave", {}).get("reopens", 0) or 0))
 fetch_b = (sum(fetch["body"]) + sum(fetch["edge"])) * 1024 * read_corr
 write_b = (sum(write["body"]) + sum(write["edge"])) * 1024 * write_corr
-waves_per_round = line["config"].get("dynamic_wave", {}).get("waves", 1) or 1
-n_rounds = rounds / max(1.0, 1.0 + line["config"].get("dynamic_wave", {}).get("reopens", 0))
 traffic = (fetch_b + write_b) / n_rounds if n_rounds else None
-# kernel-trace durations of the body launches (enqueue-independent: GPU start -> end)
-durs = []
-try:
-    for r in rows(f"{name}_trace", "run_kernel_trace.csv"):
-        if "dyn_wave_kernel" in r["Kernel_Name"] and "false" in r["Kernel_Name"].split("dyn_wave_kernel", 1)[1][:40]:
-            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-except (FileNotFoundError, KeyError):
-    pass
+# kernel-trace durations of the body launches (GPU start -> end: the arrival phase included)
+durs = per_kind(f"{name}_trace", "run_kernel_trace.csv",
+                lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)["body"]
 dyn = line["config"].get("dynamic_wave", {})
 res = {
     "tag": tag, "workload": cfg["workload"], "kernel": "dyn_wave_kernel (body + edge launches)",

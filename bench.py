@@ -1213,6 +1213,11 @@ def main_plugin(args: argparse.Namespace) -> int:
             cpu = dict(cpu, value=round(cpu["seconds_per_round"] * 1e3, 3), unit="ms per round")
     short = {"float32": "fp32", "float16": "fp16", "bfloat16": "bf16", "float64": "fp64"}[args.in_dtype]
     gbps = round(job_bytes / step_s / 1e9, 2)
+    workload = (f"{'gradient' if in_round else 'plugin'}_fedavg_{args.layout}_{short}_{N}_clients"
+                + (f"_in_{bursts}_bursts_{gap_s * 1e3:g}ms_apart" if bursts > 1 else "")
+                + (f"_waves_of_{wave}" if n_waves > 1 and not algo.wave_min else "")
+                + (f"_early_waves_from_{algo.wave_min}" if algo.wave_min else ""))
+    traffic, traffic_ratio, traffic_src = committed_dyn_traffic(workload) if dyn_rows_all else (None, None, None)
     line = {
         "metric": ("burst-cadence FedAvg round through the plugin surface (the reference server's poll-then-sleep "
                    "loop): last arrival to result latency" if burst else
@@ -1227,10 +1232,7 @@ def main_plugin(args: argparse.Namespace) -> int:
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": not (in_round or burst),
         "scaling": "replicas only", "vs_baseline": None, "dtype": "f64", "GBps": gbps,
         "data": "synthetic: client params ~ N(0,1) seeded per client, weights = dataset sizes in [100, 5000]",
-        "config": {"workload": (f"{'gradient' if in_round else 'plugin'}_fedavg_{args.layout}_{short}_{N}_clients"
-                                + (f"_in_{bursts}_bursts_{gap_s * 1e3:g}ms_apart" if bursts > 1 else "")
-                                + (f"_waves_of_{wave}" if n_waves > 1 and not algo.wave_min else "")
-                                + (f"_early_waves_from_{algo.wave_min}" if algo.wave_min else "")),
+        "config": {"workload": workload,
                    "clients": N, "params_per_client": P, "tensors_per_client": T, "in_dtype": args.in_dtype,
                    "out_dtype": args.out_dtype, "clients_per_launch": wave, "wave_min": algo.wave_min,
                    "waves_per_round": round(launches / args.steps, 2) if launches else None, "in_round": in_round,
@@ -1247,7 +1249,8 @@ def main_plugin(args: argparse.Namespace) -> int:
                                        "BASELINE.json configs[1] through the reference's plugin call sequence")},
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
+            "traffic_source": traffic_src,
             "kernel": ("dyn_wave_kernel (body launch, enqueued at the first arrival; arrivals included)"
                        if dyn_rows_all else f"fedavg_tile_kernel x {n_waves} launch(es) per round"),
             "bytes_per_step": launch_bytes,
@@ -1653,6 +1656,18 @@ def committed_traffic(world: int, n_local: int, in_dtype: str, out_dtype: str) -
         return None, None
     d = json.loads(files[-1].read_text())
     return float(d["hbm_traffic_bytes_per_launch"]), f"profiles/{files[-1].name}"
+
+
+def committed_dyn_traffic(workload: str) -> tuple[float | None, float | None, str | None]:
+    """(HBM bytes per round, ratio to algorithmic, source) of the dynamic wave for this plugin /
+    gradient workload from the newest committed PMC summary (scripts/dyn_traffic.sh ->
+    profiles/<tag>_dyn_traffic_<name>.json), or Nones."""
+    for f in sorted((REPO / "profiles").glob("r[0-9][0-9]_dyn_traffic_*.json"), reverse=True):
+        d = json.loads(f.read_text())
+        if d.get("workload") == workload and d.get("hbm_traffic_bytes_per_round"):
+            return float(d["hbm_traffic_bytes_per_round"]), round(float(d["traffic_over_algorithmic"]), 4), \
+                f"profiles/{f.name}"
+    return None, None, None
 
 
 def job_clients(args: argparse.Namespace, world: int) -> int:

@@ -2620,15 +2620,11 @@ hipError_t launch_fold_pv(const KArgs& a, int fold, int nblocks, hipStream_t s, 
   return hipGetLastError();
 }
 
-// partv: the tile table is a balanced order (pieces of whole lane-vectors: the PV instantiation).
-// FEDAVG_PARTV=0 (A/B knob) runs such tables through the general kernel instead.
-#ifndef FEDAVG_PARTV
-#define FEDAVG_PARTV 1
-#endif
+// partv: the tile table is a balanced order (pieces of whole lane-vectors: the PV instantiation)
 template <typename T, int OUT, int SPLIT, bool VEC, int TILEN = kTile1>
 hipError_t launch_fold(const KArgs& a, int fold, int nblocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                        bool partv = false) {
-  if constexpr (SPLIT == 1 && VEC && FEDAVG_PARTV != 0) {
+  if constexpr (SPLIT == 1 && VEC) {
     if (partv) return launch_fold_pv<T, OUT, SPLIT, VEC, TILEN, true>(a, fold, nblocks, s, e0, e1);
   }
   return launch_fold_pv<T, OUT, SPLIT, VEC, TILEN, false>(a, fold, nblocks, s, e0, e1);

@@ -34,3 +34,24 @@ def hand_over(payload: bytes) -> float:
     p.join(timeout=120)
     assert p.exitcode == 0, p.exitcode
     return total
+
+
+def produce(conn, shapes: dict, seeds: list) -> None:
+    """A worker process on the same GPU: makes one update per seed on cuda:0 and sends it through
+    torch.multiprocessing (CUDA IPC, what the reference's pipes do with CUDA tensors), then keeps
+    the tensors alive until the receiver says it is done."""
+    import torch
+    import torch.multiprocessing  # noqa: F401  (registers the tensor reducers)
+    from multiprocessing.reduction import ForkingPickler
+
+    dev = torch.device("cuda", 0)
+    kept = []
+    for s in seeds:
+        g = torch.Generator().manual_seed(s)
+        upd = {name: torch.randn(sh, generator=g).to(dev) for name, sh in shapes.items()}
+        kept.append(upd)
+        conn.send_bytes(bytes(ForkingPickler.dumps(upd)))
+    torch.cuda.synchronize()
+    conn.recv()  # the receiver is done with them
+    del kept
+    conn.close()

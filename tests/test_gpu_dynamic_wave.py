@@ -380,3 +380,45 @@ def test_last_rows_still_being_copied(hip_device):
     for name, v in want.items():
         assert bits_equal(got[name].cpu().numpy(), v), name
     algo.exit()
+
+
+def test_updates_from_another_process_keep_the_wave_off(hip_device):
+    # a worker process on the same GPU sends its updates as CUDA tensors (IPC): that process has a
+    # context on this GPU, so the round folds in ordinary launches (no wave holding the register
+    # file), with the same bits
+    import torch.multiprocessing as mp
+    from multiprocessing.reduction import ForkingPickler
+
+    from tests.ipc_consumer import produce
+
+    seeds = [31, 32, 33, 34, 35]
+    ctx = mp.get_context("spawn")
+    parent, child = ctx.Pipe()
+    p = ctx.Process(target=produce, args=(child, SHAPES, seeds))
+    p.start()
+    try:
+        algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+        oracle = OracleFedAvg()
+        for k, s in enumerate(seeds):
+            upd = ForkingPickler.loads(parent.recv_bytes())
+            g = torch.Generator().manual_seed(s)
+            host = {name: torch.randn(sh, generator=g) for name, sh in SHAPES.items()}
+            w = 100 + k
+            algo.process_worker_data(k, ParameterMessage(parameter=upd, aggregation_weight=w))
+            oracle.process_worker_data(k, OracleMessage(parameter={m: t.numpy() for m, t in host.items()},
+                                                        aggregation_weight=w))
+            del upd
+        got = algo.aggregate_worker_data().parameter
+        algo.clear_worker_data()
+        want = oracle.aggregate_worker_data().parameter
+        for name, v in want.items():
+            assert bits_equal(got[name].cpu().numpy(), v), name
+        assert algo.dyn_stats["waves"] == 0, algo.dyn_stats
+        algo.exit()
+        del got
+        torch.cuda.synchronize()
+    finally:
+        parent.send("done")
+        p.join(timeout=120)
+    assert p.exitcode == 0
+    torch.cuda.ipc_collect()

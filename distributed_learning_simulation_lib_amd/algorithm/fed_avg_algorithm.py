@@ -229,9 +229,8 @@ class FedAVGAlgorithm(AggregationAlgorithm):
 
     @dynamic_wave.setter
     def dynamic_wave(self, on: bool) -> None:
-        from dataclasses import replace
-
-        self.__dyn.settings = replace(self.__dyn.settings, enabled=bool(on))
+        self.settings = self.settings.with_overrides(dynamic_wave=bool(on))
+        self.__dyn.settings = self.settings.dynamic
 
     @property
     def dyn_stats(self) -> dict[str, int]:

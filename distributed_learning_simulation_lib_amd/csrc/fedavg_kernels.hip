@@ -895,6 +895,16 @@ struct DynMirror {  // device memory, written by the mirror workgroup: one copy 
   uint64_t pad[7];
 };
 constexpr int kDynCopies = 8;
+// poll back-off (s_sleep units of 64 clocks) of the mirror's host-word polls and of a waiting tile
+// workgroup's mirror-word polls (A/B knobs FEDAVG_DYN_MSLEEP / FEDAVG_DYN_TSLEEP)
+#ifndef FEDAVG_DYN_MSLEEP
+#define FEDAVG_DYN_MSLEEP 8
+#endif
+#ifndef FEDAVG_DYN_TSLEEP
+#define FEDAVG_DYN_TSLEEP 32
+#endif
+constexpr int kDynMirrorSleep = FEDAVG_DYN_MSLEEP;
+constexpr int kDynTileSleep = FEDAVG_DYN_TSLEEP;
 // the mirror word: rows mirrored (bits 0-23), closed (bit 24), close mode (bits 25-27), the wave's
 // epoch (bits 32-63: a word left by an earlier wave reads as "nothing yet", so no per-wave reset)
 __host__ __device__ constexpr uint64_t dyn_word(uint32_t count, uint32_t closed, uint32_t mode, uint32_t epoch) {
@@ -1000,7 +1010,7 @@ __device__ void dyn_mirror(const DynArgs& a) {
           st = 2;
           break;
         }
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(kDynMirrorSleep);
       }
       s_cmd[0] = hc;
       s_cmd[1] = st;
@@ -1235,7 +1245,7 @@ void dyn_wave_kernel(DynArgs a) {
             cmode = OUT_ACC;
             break;
           }
-          __builtin_amdgcn_s_sleep(32);
+          __builtin_amdgcn_s_sleep(kDynTileSleep);
         }
         // no acquire: every handed-off byte (the mirror's table) is stored and loaded with
         // system-coherent accesses, which no L1 / L2 copy can serve stale (Guideline 16's sc1

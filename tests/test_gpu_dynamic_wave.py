@@ -160,8 +160,10 @@ def test_bursts_close_reopen_close_at_the_default_idle_limit(hip_device, monkeyp
     for r in range(2):
         _round(algo, hip_device, 15, 80 + r, dtype, mutate=mutate)
     st = algo.dyn_stats
-    assert _core(st) == {"waves": 2, "rows": 30, "finalized": 2}, st
+    assert st["waves"] == 2 and st["rows"] == 30, st
     assert st["reopens"] >= 2, st  # at least one continued wave per round
+    # (a wave that ended itself after the round's last publication leaves the division to the
+    # ordinary finalize — slow hosts between arrivals: finalized may be 0-2, the bits the same)
     algo.exit()
 
 

@@ -896,15 +896,9 @@ struct DynMirror {  // device memory, written by the mirror workgroup: one copy 
 };
 constexpr int kDynCopies = 8;
 // poll back-off (s_sleep units of 64 clocks) of the mirror's host-word polls and of a waiting tile
-// workgroup's mirror-word polls (A/B knobs FEDAVG_DYN_MSLEEP / FEDAVG_DYN_TSLEEP)
-#ifndef FEDAVG_DYN_MSLEEP
-#define FEDAVG_DYN_MSLEEP 8
-#endif
-#ifndef FEDAVG_DYN_TSLEEP
-#define FEDAVG_DYN_TSLEEP 32
-#endif
-constexpr int kDynMirrorSleep = FEDAVG_DYN_MSLEEP;
-constexpr int kDynTileSleep = FEDAVG_DYN_TSLEEP;
+// workgroup's mirror-word polls; 4x and 16x shorter measured the same (profiles/r06_dyn_poll_sleep_ab.txt)
+constexpr int kDynMirrorSleep = 8;
+constexpr int kDynTileSleep = 32;
 // the mirror word: rows mirrored (bits 0-23), closed (bit 24), close mode (bits 25-27), the wave's
 // epoch (bits 32-63: a word left by an earlier wave reads as "nothing yet", so no per-wave reset)
 __host__ __device__ constexpr uint64_t dyn_word(uint32_t count, uint32_t closed, uint32_t mode, uint32_t epoch) {

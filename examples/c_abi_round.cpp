@@ -7,6 +7,8 @@
 //   4. the multi-GPU exchange on a one-rank RCCL world: fedavg_comm_* + fedavg_sharded_round
 //      (reduce to the root) and fedavg_sharded_round_scatter (reduce-scatter + window finalize +
 //      gather)
+//   5. the round folded while it arrives, in two bursts (fedavg_dyn_*: the wave ends itself in
+//      the pause and is continued from the fp64 accumulator by the next publication)
 //
 // Self-check: the streamed result and the sharded result are compared bit-for-bit with a plain
 // fp64 host fold in arrival order (acc = -0.0; acc += double(x) * w; out = acc / W) — the
@@ -14,6 +16,7 @@
 // library (_lib/c_abi_round), run by tests/test_gpu_c_abi.py.
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <cinttypes>
 #include <cstdint>
 #include <cstdio>
@@ -156,6 +159,39 @@ int main() {
     CHECK_ST(fedavg_check(ctx, stream, nullptr));
     if (compare(round == 0 ? "scatter round 1" : "scatter round 2")) return 1;
   }
+
+  // (3) the round folded while it arrives (fedavg_dyn_*), at the reference server's burst cadence:
+  //     4 updates, a pause longer than the wave's idle limit (it ends itself, its rows kept in the
+  //     fp64 accumulator), the other 5 — the next publication continues the wave from the
+  //     accumulator — then the close divides into the outputs
+  CHECK_ST(fedavg_reset(ctx, stream));
+  CHECK_HIP(hipStreamSynchronize(stream));
+  CHECK_ST(fedavg_dyn_configure(ctx, 300, 0));  // idle limit 300 us
+  for (int t = 0; t < T; ++t) CHECK_HIP(hipMemset(out[t], 0xFF, numel[t] * sizeof(double)));
+  CHECK_ST(fedavg_dyn_open(ctx, FEDAVG_F32, N, stream));
+  int32_t published = 0;
+  CHECK_ST(fedavg_dyn_publish(ctx, dev.data(), wtab.data(), 4, stream, &published));
+  if (published != 4) {
+    std::fprintf(stderr, "dynamic wave: %d of 4 rows published\n", (int)published);
+    return 1;
+  }
+  {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(5);
+    while (std::chrono::steady_clock::now() < until) {
+    }
+  }
+  CHECK_ST(fedavg_dyn_publish(ctx, dev.data(), wtab.data(), N, stream, &published));
+  int32_t info[5] = {0, 0, 0, 0, 0};
+  CHECK_ST(fedavg_dyn_info(ctx, info, 5));
+  int32_t folded = 0, finalized = 0;
+  CHECK_ST(fedavg_dyn_close(ctx, out.data(), FEDAVG_F64, 1, stream, &folded, &finalized));
+  CHECK_ST(fedavg_check(ctx, stream, nullptr));
+  if (folded != N || !finalized || info[2] != 4 || info[3] < 1) {
+    std::fprintf(stderr, "dynamic wave: folded %d finalized %d base %d continued %d\n", (int)folded, (int)finalized,
+                 (int)info[2], (int)info[3]);
+    return 1;
+  }
+  if (compare("dynamic wave in two bursts (continued once)")) return 1;
 
   CHECK_ST(fedavg_comm_destroy(comm));
   CHECK_ST(fedavg_plan_destroy(partial));

@@ -428,3 +428,35 @@ def test_updates_from_another_process_keep_the_wave_off(hip_device):
         p.join(timeout=120)
     assert p.exitcode == 0
     torch.cuda.ipc_collect()
+
+
+def test_device_round_then_host_rounds(hip_device):
+    # a round of device-resident updates (wave), then rounds whose updates arrive in host memory:
+    # those fold in ordinary launches and no wave is pre-opened for them (nothing would bind it);
+    # a later device round opens one again. Every round bit-identical.
+    algo = FedAVGAlgorithm(device=hip_device, dynamic_wave=True)
+    _round(algo, hip_device, 6, 60)
+    assert algo.dyn_stats["waves"] == 1
+
+    def host_round(seed):
+        g = torch.Generator().manual_seed(seed)
+        oracle = OracleFedAvg()
+        for k in range(5):
+            p = {name: torch.randn(s, generator=g) for name, s in SHAPES.items()}
+            w = 50 + 7 * k
+            algo.process_worker_data(k, ParameterMessage(parameter=dict(p), aggregation_weight=w))
+            oracle.process_worker_data(k, OracleMessage(parameter={m: t.numpy() for m, t in p.items()},
+                                                        aggregation_weight=w))
+        got = algo.aggregate_worker_data().parameter
+        algo.clear_worker_data()
+        for name, v in oracle.aggregate_worker_data().parameter.items():
+            assert bits_equal(got[name].cpu().numpy(), v), name
+
+    launches0 = algo._context().dyn_info()["launches"]
+    host_round(61)
+    host_round(62)
+    assert algo.dyn_stats["waves"] == 1, algo.dyn_stats
+    assert algo._context().dyn_info()["launches"] == launches0  # no pre-opened wave either
+    _round(algo, hip_device, 6, 63)
+    assert algo.dyn_stats["waves"] == 2, algo.dyn_stats
+    algo.exit()

@@ -387,7 +387,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         worker_data: Message | None,
     ) -> bool:
         self.__round_updates += 1
-        if self.__round_updates == 1:
+        if self.__round_updates == 1 and self._device_update(worker_data):
             self.__dyn.preopen(self._context, self._dyn_eligible(), self.__table is not None, self.wave_size)
         if worker_data is not None and self._arrive_quick(worker_id, worker_data):
             return True
@@ -956,6 +956,16 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             dyn.arrival(self.__table, self._context,
                         self._dyn_eligible() and self.__ew is False and not self._shared_device(probe),
                         self.__table_dtype, self.wave_size)
+
+    @staticmethod
+    def _device_update(worker_data: Any) -> bool:
+        """The update's first tensor is already on a GPU (a round that may take a wave: host
+        updates never do, so no wave is opened ahead of them)."""
+        payload = getattr(worker_data, "parameter", None)
+        if not isinstance(payload, dict) or not payload:
+            return False
+        first = next(iter(payload.values()))
+        return isinstance(first, torch.Tensor) and first.is_cuda
 
     @staticmethod
     def _shared_device(t: Any) -> bool:

@@ -33,7 +33,9 @@ def _patient_wave(monkeypatch):
 SHAPES = {"conv": (16, 3, 5, 5), "bias": (16,), "fc": (10, 700), "big": (3, 4096), "tail": (4096 + 37,)}
 
 
-def _round(algo, dev, n, seed, dtype=torch.float32, weights="int", mutate=None):
+def _round(algo, dev, n, seed, dtype=torch.float32, weights="int", mutate=None, settle=False):
+    """One plugin round against the oracle; ``settle``: the copies of each update are finished
+    before it is handed over (every publication then takes its rows at once)."""
     g = torch.Generator().manual_seed(seed)
     rng = np.random.default_rng(seed)
     oracle = OracleFedAvg()
@@ -42,8 +44,10 @@ def _round(algo, dev, n, seed, dtype=torch.float32, weights="int", mutate=None):
         if mutate is not None:
             p = mutate(k, p)
         w = int(rng.integers(100, 5000)) if weights == "int" else float(rng.uniform(0.1, 3.0))
-        algo.process_worker_data(k, ParameterMessage(parameter={m: t.to(dev) for m, t in p.items()},
-                                                     aggregation_weight=w))
+        upd = {m: t.to(dev) for m, t in p.items()}
+        if settle:
+            torch.cuda.current_stream(dev).synchronize()
+        algo.process_worker_data(k, ParameterMessage(parameter=upd, aggregation_weight=w))
         arrs = {m: (t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy())
                 for m, t in p.items()}
         oracle.process_worker_data(k, OracleMessage(parameter=arrs, aggregation_weight=w,
@@ -182,7 +186,7 @@ def test_idle_before_the_aggregate_finalizes_from_the_accumulator(hip_device, mo
     algo.aggregate_worker_data = late
     # 5 rows: published at once, then in pairs — every row is out before the sleep (an unpublished
     # last row would instead be handed to a continued wave, which then divides: the other test)
-    _round(algo, hip_device, 5, 90)
+    _round(algo, hip_device, 5, 90, settle=True)
     st = algo.dyn_stats
     # every row folded by waves; the 10 ms sleep ends the last one before the close, which then
     # finalizes from the accumulator (a slow host may also see waves end between arrivals: they
